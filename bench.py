@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""Benchmark: candidate N-step rollouts/s + MPC-step p50 latency (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU)
+
+Workloads:
+  C (default)  N=10 horizon, 1e6 candidates per GPU, moving-target episode
+               (reference operator schedule), grid regenerated per step and
+               sampled on device; weak scaling: 1e6 x G candidates over G GPUs
+  B            N=3, 1e5 candidates per GPU, same episode machinery
+  D            N=12, 1.25e6 candidates per GPU (1e7 over 8), one exchange/step
+  E            1024 robots x 1e4 candidates, N=8, batched per-robot arg-min,
+               robots sharded over GPUs (128 per GPU at 8), no exchange
+
+A "step" is one MPC step: host grid -> device sampler -> rollout kernel ->
+finalize -> [RCCL exchange] -> 808-B winner read -> host episode update.
+Controls never leave HBM; inputs to the timed region are device-resident.
+
+Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel
+(k_rollout_argmin): algorithmic bytes 16 B per candidate-step (fp64 v and
+beta read once) / its average duration from HIP events on the launch stream.
+`cpu_baseline` is the reference-structured Python port (scipy quad) on this
+host's cores, rank 0 at N=1 only, on a bounded sample of the same candidates;
+it runs before the GPU is initialised (it forks worker processes).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "candidate N-step rollouts/sec + MPC-step p50 latency, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+WORKLOADS = {
+    "B": dict(n_steps=3, per_gpu=100_000, desc="config B: N=3, 1e5 candidates/GPU, episode"),
+    "C": dict(n_steps=10, per_gpu=1_000_000,
+              desc="config C: N=10, 1e6 candidates/GPU, moving-target episode"),
+    "D": dict(n_steps=12, per_gpu=1_250_000,
+              desc="config D: N=12, 1.25e6 candidates/GPU (1e7 at 8 GPUs), RCCL exchange"),
+    "E": dict(n_steps=8, per_gpu=None, robots=1024, cand=10_000,
+              desc="config E: 1024 robots x 1e4 candidates, N=8, batched per-robot arg-min"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="C", choices=sorted(WORKLOADS))
+    ap.add_argument("--integrator", default="rect", choices=["rect", "qk21"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="per-core time budget of the cpu_baseline sample (0 = skip)")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC-derived HBM bytes per launch for the roofline 'traffic' field")
+    return ap.parse_args()
+
+
+def cpu_baseline(wl, seconds):
+    """Reference-structured Python port on host cores (before GPU init)."""
+    import numpy as np
+    from diplomjourney_amd import math_model_tree as mmt
+    from oracle import cpu_ref
+    from oracle import oracle as O
+    V = mmt.vector_of_velocities(0.0)
+    B = mmt.vector_of_beta_angles(0.0)
+    n_steps = wl["n_steps"]
+    n = 400_000
+    v, b = O.sample_controls(V, B, n, n_steps, seed=20261015 + 0x9E3779B9 * 1001)
+    prob = (0.0, 0.0, 0.0, 2, 3, 0, 0, 0.5, 0.05, 0.1)
+    r = cpu_ref.timed_rate(prob, v, b, budget_s=seconds)
+    return {"value": r["rate"], "unit": "rollouts/s", "cores": r["cores"], "kind": "port",
+            "sample": (f"{r['candidates']} sampled N={n_steps} candidates of the first MPC step "
+                       f"(reference grid around v=0, beta=0), scipy.integrate.quad per "
+                       f"integral as math_model_tree.py:91-115, {r['cores']} processes x "
+                       f"{seconds:.0f} s budget, busy {r['busy_s']:.1f} s")}
+
+
+def main():
+    args = parse()
+    wl = WORKLOADS[args.workload]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(wl, args.cpu_seconds)
+
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    group = None
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+    from diplomjourney_amd.expansion import Expansion
+    eng = Expansion(device)
+
+    if args.workload == "E":
+        return bench_robots(args, wl, eng, rank, world, cpu)
+
+    from diplomjourney_amd.episode import Episode, percentile
+    n_total = wl["per_gpu"] * world
+    ep = Episode(eng, n_total, wl["n_steps"], rank=rank, world=world,
+                 integrator=args.integrator, group=group)
+    for _ in range(args.warmup):
+        ep.step()
+    ep.kernel_ms.clear()
+    ep.step_ms.clear()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ep.step(time_kernel=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = sum(ep.kernel_ms) / len(ep.kernel_ms)
+    bytes_launch = 16.0 * wl["n_steps"] * ep.n_local
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    value = n_total * args.steps / elapsed
+    out = {
+        "metric": METRIC, "value": value, "unit": "rollouts/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": wl["desc"], "n_steps": wl["n_steps"],
+                   "candidates_per_gpu": ep.n_local, "candidates_total": n_total,
+                   "integrator": args.integrator, "episodes_started": ep.episodes,
+                   "parallelism": f"candidate-sharded x{world}" + (", all_gather(808 B)/step"
+                                                                   if world > 1 else "")},
+        "p50_ms": percentile(ep.step_ms, 50), "p90_ms": percentile(ep.step_ms, 90),
+        "kernel_ms": kern_ms,
+        "roofline": roofline(achieved, bytes_launch, args.traffic_json),
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def roofline(achieved, bytes_launch, traffic_json):
+    traffic = None
+    if traffic_json and os.path.exists(traffic_json):
+        with open(traffic_json) as fh:
+            traffic = json.load(fh).get("hbm_bytes_per_launch")
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel": "k_rollout_argmin", "algorithmic_bytes_per_launch": bytes_launch}
+
+
+def bench_robots(args, wl, eng, rank, world, cpu):
+    """Config E: robots sharded over ranks, one batched launch per step."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.abi import make_problem, PROBLEM_BYTES
+    from diplomjourney_amd.distributed import shard_range
+    from diplomjourney_amd.episode import percentile
+    from diplomjourney_amd.expansion import problems_to_device, results_from_device
+    R_total, cand, n_steps = wl["robots"], wl["cand"], wl["n_steps"]
+    lo, hi = shard_range(R_total, rank, world)
+    R = hi - lo
+    probs = []
+    for r in range(lo, hi):
+        g = np.random.default_rng(20261015 + r)              # PCG64 per robot
+        x0, y0 = g.uniform(-10, 10, 2)
+        phi0 = g.uniform(-math.pi, math.pi)
+        xt, yt = g.uniform(x0 - 10, x0 + 10), g.uniform(y0 - 10, y0 + 10)
+        probs.append(make_problem(x0, y0, phi0, xt, yt, x0, y0, mmt.L, 0.05, 0.1))
+    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device=eng.device)
+    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device=eng.device)
+    v = torch.empty((n_steps, R * cand), dtype=torch.float64, device=eng.device)
+    b = torch.empty_like(v)
+    for i in range(R):
+        eng.sample_controls(V, B, cand, n_steps, 20261015 + lo + i, v_out=v[:, i * cand:],
+                            beta_out=b[:, i * cand:], ld=R * cand)
+    probs_dev = problems_to_device(probs, eng.device)
+    out = torch.zeros(R * eng.result.numel(), dtype=torch.uint8, device=eng.device)
+    host = torch.empty(out.numel(), dtype=torch.uint8).pin_memory()
+    step_ms, kern = [], []
+    state = torch.empty((R, 3), dtype=torch.float64)
+
+    def one(timed):
+        t0 = time.perf_counter()
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        eng.rollout_argmin_batched(probs_dev, v, b, cand, integrator=args.integrator, out=out)
+        if timed:
+            e1.record()
+        host.copy_(out, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        if timed:
+            kern.append(e0.elapsed_time(e1))
+        step_ms.append((time.perf_counter() - t0) * 1e3)
+
+    for _ in range(args.warmup):
+        one(False)
+    step_ms.clear()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=eng.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    res = results_from_device(out)
+    assert all(r.index >= 0 for r in res)
+    kern_ms = sum(kern) / len(kern)
+    bytes_launch = 16.0 * n_steps * R * cand
+    outd = {
+        "metric": METRIC, "value": R_total * cand * args.steps / elapsed, "unit": "rollouts/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": wl["desc"], "n_steps": n_steps, "robots_per_gpu": R,
+                   "candidates_per_robot": cand, "integrator": args.integrator,
+                   "parallelism": f"robot-sharded x{world}, no exchange"},
+        "p50_ms": percentile(step_ms, 50), "kernel_ms": kern_ms,
+        "roofline": roofline(bytes_launch / (kern_ms * 1e-3) / 1e9, bytes_launch,
+                             args.traffic_json),
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(outd), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

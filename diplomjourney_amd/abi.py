@@ -1,0 +1,83 @@
+"""ctypes mirror of include/mpc_rollout.h (structs, constants, status codes).
+
+Kept in one place so the product binding (`native.py`) and the test-side
+oracle binding agree on the byte layout.  Layout is checked against the C
+compiler's sizeof/offsetof in tests/test_abi.py.
+"""
+import ctypes
+
+MPC_MAX_STEPS = 32
+
+MPC_OK = 0
+MPC_ERR_ARG = -1
+MPC_ERR_WORKSPACE = -2
+MPC_ERR_HIP = -3
+MPC_ERR_UNSUPPORTED = -4
+
+MPC_INTEG_QK21 = 0
+MPC_INTEG_RECT = 1
+
+INTEGRATORS = {"qk21": MPC_INTEG_QK21, "rect": MPC_INTEG_RECT}
+
+
+class MpcProblem(ctypes.Structure):
+    """mpc_problem_t: one robot at one MPC step (math_model_tree.py:278-306)."""
+    _fields_ = [
+        ("x", ctypes.c_double), ("y", ctypes.c_double), ("phi", ctypes.c_double),
+        ("x_t", ctypes.c_double), ("y_t", ctypes.c_double),
+        ("x_0", ctypes.c_double), ("y_0", ctypes.c_double),
+        ("L", ctypes.c_double),
+        ("t_a", ctypes.c_double), ("t_b", ctypes.c_double),
+    ]
+
+    def as_tuple(self):
+        return tuple(getattr(self, n) for n, _ in self._fields_)
+
+
+class MpcResult(ctypes.Structure):
+    """mpc_result_t: the selected candidate and its per-step states."""
+    _fields_ = [
+        ("cost", ctypes.c_double),
+        ("index", ctypes.c_int64),
+        ("found", ctypes.c_int32),
+        ("n_steps", ctypes.c_int32),
+        ("v", ctypes.c_double),
+        ("beta", ctypes.c_double),
+        ("traj", (ctypes.c_double * 3) * MPC_MAX_STEPS),
+    ]
+
+    def trajectory(self):
+        return [[self.traj[s][k] for k in range(3)] for s in range(self.n_steps)]
+
+    def as_dict(self):
+        return {"cost": self.cost, "index": self.index, "found": bool(self.found),
+                "n_steps": self.n_steps, "v": self.v, "beta": self.beta,
+                "traj": self.trajectory()}
+
+
+RESULT_BYTES = ctypes.sizeof(MpcResult)
+PROBLEM_BYTES = ctypes.sizeof(MpcProblem)
+
+STATUS_TEXT = {
+    MPC_OK: "ok",
+    MPC_ERR_ARG: "invalid argument",
+    MPC_ERR_WORKSPACE: "workspace too small",
+    MPC_ERR_HIP: "HIP runtime error",
+    MPC_ERR_UNSUPPORTED: "unsupported option",
+}
+
+
+class MpcError(RuntimeError):
+    def __init__(self, status, where=""):
+        self.status = status
+        super().__init__(f"{where}: status {status} ({STATUS_TEXT.get(status, 'unknown')})")
+
+
+def result_from_bytes(buf):
+    """Decode one mpc_result_t from a bytes-like object (e.g. a CPU uint8 tensor)."""
+    return MpcResult.from_buffer_copy(bytes(buf))
+
+
+def make_problem(x, y, phi, x_t, y_t, x_0, y_0, L, t_a, t_b):
+    return MpcProblem(float(x), float(y), float(phi), float(x_t), float(y_t),
+                      float(x_0), float(y_0), float(L), float(t_a), float(t_b))

@@ -1,0 +1,123 @@
+// mpc_device.h — device-side arithmetic of the MPC candidate expansion (gfx950).
+//
+// Every function here states one piece of ShittyWizard/DiplomJourney's
+// math_model_tree.py in IEEE fp64 with the reference's operation order.  The
+// translation unit is compiled with -ffp-contract=off so each + - * / is one
+// rounding, exactly as in CPython; tan/sincos/sqrt are the ROCm device
+// library's fp64 routines (faithfully rounded, <= 1 ulp from glibc's).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mpc_rollout.h"
+
+namespace mpc {
+
+// Per-problem constants, derived once on the host (or per robot on device).
+struct Consts {
+  double x, y, phi;        // s0 = initial_coordinates (math_model_tree.py:294)
+  double x_t, y_t;         // target globals (:65-66)
+  double x_0, y_0;         // line origin globals (:57)
+  double A, B, C1, C2;     // (y_t-y_0), (x_t-x_0), x_t*y_0, y_t*x_0   (:60)
+  double den;              // sqrt((y_t-y_0)**2 + (x_t-x_0)**2)        (:61)
+  double L, inv_L;         // wheelbase; 1/L when L is a power of two
+  double h;                // (t+dt) - t, the quad interval length (RECT)
+  double hlgth;            // 0.5*((t+dt) - t), QUADPACK's half length (QK21)
+  int32_t L_pow2;          // v/L == v*inv_L exactly
+  int32_t pad_;
+};
+
+// QUADPACK dqk21 Kronrod weights wgk(1..11).
+__device__ constexpr double kWGK[11] = {
+    0.011694638867371874278064396062192, 0.032558162307964727478818972459390,
+    0.054755896574351996031381300244580, 0.075039674810919952767043140916190,
+    0.093125454583697605535065465083366, 0.109387158802297641899210590325805,
+    0.123491976262065851077208698889469, 0.134709217311473325928054001771707,
+    0.142775938577060080797094273138717, 0.147739104901338491374841515972068,
+    0.149445554002916905664936468389821};
+
+// sp.quad(f, t, t+dt) of a constant integrand (math_model_tree.py:91-96).
+template <int INTEG>
+__device__ __forceinline__ double quad_const(double f, const Consts& K) {
+  if constexpr (INTEG == MPC_INTEG_RECT) {
+    return f * K.h;
+  } else {
+    double resk = kWGK[10] * f;
+    const double fsum = f + f;
+#pragma unroll
+    for (int j = 1; j <= 9; j += 2) resk = resk + kWGK[j] * fsum;
+#pragma unroll
+    for (int j = 0; j <= 8; j += 2) resk = resk + kWGK[j] * fsum;
+    return resk * K.hlgth;
+  }
+}
+
+// iteration_of_predict (math_model_tree.py:111-115): heading first, then
+// position with the updated heading (semi-implicit bicycle step).
+template <int INTEG>
+__device__ __forceinline__ void step(double& x, double& y, double& ph, double v, double beta,
+                                     const Consts& K) {
+  const double w = K.L_pow2 ? v * K.inv_L : v / K.L;          // _velocity / L   (:78)
+  const double dphi = quad_const<INTEG>(w * tan(beta), K);     // angle_phi       (:107)
+  ph = ph + dphi;                                              // phi + _phi      (:113)
+  double s, c;
+  sincos(ph, &s, &c);
+  x = x + quad_const<INTEG>(v * c, K);                         // coordinate_x    (:99)
+  y = y + quad_const<INTEG>(v * s, K);                         // coordinate_y    (:103)
+}
+
+// control_criterion (math_model_tree.py:82-87) on the layer-N state.
+__device__ __forceinline__ double cost(double x, double y, const Consts& K) {
+  const double ex = K.x_t - x, ey = K.y_t - y;
+  const double dist_target = sqrt(ex * ex + ey * ey);          // :66
+  double d;
+  if (x == K.x_0 && y == K.y_0) {
+    d = 1000.0;                                                // :57-58
+  } else {
+    d = fabs(K.A * x - K.B * y + K.C1 - K.C2) / K.den;         // :60-61
+  }
+  return 10000.0 * dist_target + 10000.0 * (d * d);            // :62, :87
+}
+
+// Total order on costs for the arg-min: non-finite costs (NaN, +inf) map to
+// the largest key and never win; -0 is folded into +0.
+__device__ __forceinline__ uint64_t cost_key(double c) {
+  if (!(c < __builtin_inf())) return ~0ull;
+  c = c + 0.0;
+  const uint64_t u = static_cast<uint64_t>(__double_as_longlong(c));
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+
+__device__ __forceinline__ double key_cost(uint64_t k) {
+  if (k == ~0ull) return __builtin_inf();
+  const uint64_t u = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+  return __longlong_as_double(static_cast<long long>(u));
+}
+
+// Lexicographic (key, index) order: lowest cost, then lowest index — the
+// first strict minimum of the reference's ascending scan (:351).
+__device__ __forceinline__ bool rec_less(uint64_t ka, int64_t ia, uint64_t kb, int64_t ib) {
+  return ka < kb || (ka == kb && ia < ib);
+}
+
+__device__ __forceinline__ void wave_argmin(uint64_t& k, int64_t& i) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t ok = __shfl_xor(k, off, 64);
+    const int64_t oi = __shfl_xor(i, off, 64);
+    if (rec_less(ok, oi, k, i)) {
+      k = ok;
+      i = oi;
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+}  // namespace mpc

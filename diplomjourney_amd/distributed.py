@@ -1,0 +1,62 @@
+"""Candidate sharding and the per-MPC-step winner exchange.
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).
+Rank g owns the contiguous candidate range [g*C/G, (g+1)*C/G); its kernel
+reports global indices (index_base), so the lowest-index tie-break is the same
+as on one device and in the reference's ascending scan.
+
+RCCL has no (min, index) reduction, so the exchange is ONE all_gather of the
+per-rank 808-byte result records (cost, global index, found, winner
+trajectory) followed by the lexicographic (cost, index) selection on every
+rank — semantically the all-reduce(min+index) of the north star, and it
+carries the winner's trajectory in the same collective, so no second
+broadcast is needed.  The payload is G x 808 B: pure latency over xGMI.
+"""
+import math
+
+import torch
+import torch.distributed as dist
+
+from .abi import RESULT_BYTES, MpcResult
+
+
+def shard_range(n_total, rank, world):
+    """Contiguous [lo, hi) of candidate indices owned by `rank`."""
+    base, rem = divmod(n_total, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def gather_results(local_out, group=None):
+    """all_gather of one uint8[RESULT_BYTES] record per rank -> uint8[world*RESULT_BYTES]."""
+    world = dist.get_world_size(group)
+    gathered = torch.empty(world * RESULT_BYTES, dtype=torch.uint8, device=local_out.device)
+    dist.all_gather_into_tensor(gathered, local_out, group=group)
+    return gathered
+
+
+def _key(res):
+    """Total order used on device (mpc_device.h cost_key): non-finite or
+    missing winners last, then cost, then global index."""
+    if res.index < 0 or not (res.cost < math.inf):
+        return (1, 0.0, 0)
+    return (0, res.cost + 0.0, res.index)
+
+
+def select_winner_host(records, incumbent=math.inf):
+    """Host restatement of k_select_winner for CPU process groups (gloo) and
+    tests: records is a list of MpcResult (or a bytes blob of them)."""
+    if isinstance(records, (bytes, bytearray, memoryview)):
+        raw = bytes(records)
+        records = [MpcResult.from_buffer_copy(raw[i:i + RESULT_BYTES])
+                   for i in range(0, len(raw), RESULT_BYTES)]
+    best = min(range(len(records)), key=lambda r: _key(records[r]))
+    out = MpcResult.from_buffer_copy(bytes(records[best]))
+    out.found = int(_key(out)[0] == 0 and out.cost < incumbent)
+    return out
+
+
+def exchange_winner(engine, local_out, incumbent=math.inf, group=None):
+    """Device path: all_gather (RCCL) + on-device selection into engine.result."""
+    gathered = gather_results(local_out, group)
+    return engine.select_winner(gathered, incumbent=incumbent)

@@ -1,0 +1,110 @@
+"""ctypes binding of the HIP library libmpc_rollout.so (include/mpc_rollout.h).
+
+The product path has no CPU fallback: if the in-tree library is missing or a
+call returns a non-zero status, this module raises.  Device buffers come from
+PyTorch-ROCm tensors (`tensor.data_ptr()`), the stream from
+`torch.cuda.current_stream().cuda_stream`.  torch is imported first so the
+library's libamdhip64.so.7 dependency resolves to the runtime torch already
+loaded (one HIP runtime per process).
+"""
+import ctypes
+import os
+import subprocess
+import sys
+
+from .abi import MpcError, MpcProblem
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_NAME = "libmpc_rollout.so"
+LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
+# Developer override for A/B-testing kernel variants built elsewhere.
+_LIB_OVERRIDE = os.environ.get("DIPLOMJOURNEY_MPC_LIB")
+SRC = os.path.join(PKG_DIR, "csrc", "mpc_rollout.hip")
+HEADER = os.path.join(REPO_DIR, "include", "mpc_rollout.h")
+
+# Every symbol include/mpc_rollout.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "mpc_version", "mpc_strerror", "mpc_workspace_bytes", "mpc_rollout_argmin",
+    "mpc_rollout_partials", "mpc_rollout_finalize",
+    "mpc_batched_workspace_bytes", "mpc_rollout_argmin_batched", "mpc_select_winner",
+    "mpc_sample_controls",
+)
+
+HIPCC_FLAGS = [
+    "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+    # One IEEE rounding per reference operator: no a*b+c contraction.
+    "-ffp-contract=off",
+    "-Wall",
+]
+
+
+def build(verbose=False):
+    """Compile csrc/*.hip for gfx950 into the in-tree shared library."""
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, *HIPCC_FLAGS, "-I", os.path.join(REPO_DIR, "include"), "-o", LIB_PATH, SRC]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return LIB_PATH
+
+
+def needs_build():
+    if not os.path.exists(LIB_PATH):
+        return True
+    lib_m = os.path.getmtime(LIB_PATH)
+    srcs = [HEADER] + [os.path.join(PKG_DIR, "csrc", f) for f in os.listdir(os.path.join(PKG_DIR, "csrc"))]
+    return any(os.path.getmtime(s) > lib_m for s in srcs)
+
+
+_lib = None
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_D = ctypes.c_double
+
+
+def lib():
+    """Load the HIP library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  (one HIP runtime: torch's libamdhip64.so.7)
+    path = _LIB_OVERRIDE or LIB_PATH
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: run __graft_entry__.build() "
+                           "(the MPC expansion has no CPU fallback)")
+    L = ctypes.CDLL(path)
+    L.mpc_version.restype = ctypes.c_char_p
+    L.mpc_version.argtypes = []
+    L.mpc_strerror.restype = ctypes.c_char_p
+    L.mpc_strerror.argtypes = [ctypes.c_int]
+    L.mpc_workspace_bytes.restype = ctypes.c_size_t
+    L.mpc_workspace_bytes.argtypes = [_I64, _I32]
+    L.mpc_rollout_argmin.restype = ctypes.c_int
+    L.mpc_rollout_argmin.argtypes = [ctypes.POINTER(MpcProblem), _P, _P, _I64, _I32, _I64, _D,
+                                     _I32, _P, _P, ctypes.c_size_t, _P, _P]
+    L.mpc_rollout_partials.restype = ctypes.c_int
+    L.mpc_rollout_partials.argtypes = [ctypes.POINTER(MpcProblem), _P, _P, _I64, _I32, _I32, _P,
+                                       _P, ctypes.c_size_t, _P]
+    L.mpc_rollout_finalize.restype = ctypes.c_int
+    L.mpc_rollout_finalize.argtypes = [ctypes.POINTER(MpcProblem), _P, _P, _I64, _I32, _I64, _D,
+                                       _I32, _I32, _P, ctypes.c_size_t, _P, _P]
+    L.mpc_batched_workspace_bytes.restype = ctypes.c_size_t
+    L.mpc_batched_workspace_bytes.argtypes = [_I32, _I64, _I32]
+    L.mpc_rollout_argmin_batched.restype = ctypes.c_int
+    L.mpc_rollout_argmin_batched.argtypes = [_P, _P, _I32, _P, _P, _I64, _I32, _I32, _P,
+                                             ctypes.c_size_t, _P, _P]
+    L.mpc_select_winner.restype = ctypes.c_int
+    L.mpc_select_winner.argtypes = [_P, _I32, _D, _P, _P]
+    L.mpc_sample_controls.restype = ctypes.c_int
+    L.mpc_sample_controls.argtypes = [_P, _I32, _P, _I32, _I64, _I32, ctypes.c_uint64, _I64,
+                                      _I32, _P, _P, _I64, _P]
+    _lib = L
+    return L
+
+
+def check(status, where):
+    if status != 0:
+        raise MpcError(status, where)

@@ -1,0 +1,139 @@
+/*
+ * mpc_rollout.h — C ABI of the MI355X-native MPC candidate expansion.
+ *
+ * Drop-in boundary for ShittyWizard/DiplomJourney's hot path:
+ * the body of `predictive_control` in math_model_tree.py:278-362 — roll the
+ * bicycle-kinematic step (math_model_tree.py:69-115) forward over an N-step
+ * horizon for every candidate control sequence, score the layer-N state with
+ * `control_criterion` (:56-87) and keep the first strict minimum (:351-359).
+ *
+ * The reference has no FFI (it is pure Python); these entry points are what
+ * its Python host binds through ctypes.  Plain pointers and
+ * sizes only: every device buffer is owned by the caller, borrowed for the
+ * call, never retained.  No function throws or aborts; all return an int
+ * status (MPC_OK = 0, negative on error, see mpc_strerror).
+ *
+ * Data layout in HBM (SoA, step-major, fp64):
+ *   v_sc[s * n_cand + c], beta_sc[s * n_cand + c]   s < n_steps, c < n_cand
+ * Candidate c's global index is index_base + c (contiguous shards across GPUs).
+ */
+#ifndef DIPLOMJOURNEY_AMD_MPC_ROLLOUT_H
+#define DIPLOMJOURNEY_AMD_MPC_ROLLOUT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* mpc_stream_t; /* == hipStream_t */
+
+#define MPC_MAX_STEPS 32
+
+enum {
+  MPC_OK = 0,
+  MPC_ERR_ARG = -1,         /* bad size / null pointer / n_steps out of range   */
+  MPC_ERR_WORKSPACE = -2,   /* ws_bytes < required                              */
+  MPC_ERR_HIP = -3,         /* a HIP runtime call failed (launch, copy)         */
+  MPC_ERR_UNSUPPORTED = -4  /* e.g. integrator id unknown                       */
+};
+
+/* How the constant integrand of each quad() call is integrated.
+ * QK21: bit-faithful emulation of scipy.integrate.quad -> QUADPACK qk21 on a
+ *       constant integrand (math_model_tree.py:91-96; SURVEY Fact 4).
+ * RECT: the exact integral f*(t_b - t_a) of the constant integrand.        */
+enum { MPC_INTEG_QK21 = 0, MPC_INTEG_RECT = 1 };
+
+/* One MPC problem (one robot at one MPC step). */
+typedef struct mpc_problem {
+  double x, y, phi;   /* initial_coordinates, math_model_tree.py:294            */
+  double x_t, y_t;    /* target globals read by the cost, :56-66                */
+  double x_0, y_0;    /* line-origin globals, :57-61                            */
+  double L;           /* wheelbase, config.py:6 (v_phi, :77-78)                 */
+  double t_a, t_b;    /* quad limits [t, t + delta_t], :99-108 (t advanced :302) */
+} mpc_problem_t;
+
+/* The selected candidate.  `found` == 0 means no candidate beat `incumbent`
+ * (strict <, :351): the caller keeps its stale trajectory. */
+typedef struct mpc_result {
+  double cost;                      /* control_criterion of the winner         */
+  int64_t index;                    /* global index, -1 when no finite cost    */
+  int32_t found;                    /* cost < incumbent                        */
+  int32_t n_steps;
+  double v, beta;                   /* winner's step-0 control (:357-358)      */
+  double traj[MPC_MAX_STEPS][3];    /* (x, y, phi) after each step (:353-356)  */
+} mpc_result_t;
+
+const char* mpc_version(void);
+const char* mpc_strerror(int status);
+
+/* Workspace for mpc_rollout_argmin (per-block partial arg-min records). */
+size_t mpc_workspace_bytes(int64_t n_cand, int32_t n_steps);
+
+/*
+ * Expansion + arg-min of one problem: replaces math_model_tree.py:295-360
+ * (CoordinateTree fill + layer loops + strict-< scan) for n_steps layers.
+ *   p           host pointer, read during the call only
+ *   states_out  optional device buffer [n_steps][3][n_cand] (x, y, phi of every
+ *               candidate after every step: the CoordinateTree payload); NULL
+ *               skips it (the benchmark path)
+ *   out         device pointer to one mpc_result_t, written on `stream`
+ * Ties resolve to the lowest global index, NaN costs never win.
+ */
+int mpc_rollout_argmin(const mpc_problem_t* p, const double* v_sc, const double* beta_sc,
+                       int64_t n_cand, int32_t n_steps, int64_t index_base, double incumbent,
+                       int32_t integrator, double* states_out, void* ws, size_t ws_bytes,
+                       mpc_result_t* out, mpc_stream_t stream);
+
+/* The two launches mpc_rollout_argmin enqueues, exposed separately so a
+ * caller can time the streaming kernel alone (bench.py) or interleave other
+ * work (an exchange) between them.  Same arguments and semantics:
+ *   phase 1  mpc_rollout_partials: rollout + cost + per-block arg-min records
+ *            into ws (the HBM-streaming kernel)
+ *   phase 2  mpc_rollout_finalize: block records -> winner, winner re-rolled
+ *            into *out
+ * states_out is only accepted by phase 1 (NULL in phase 2's contract). */
+int mpc_rollout_partials(const mpc_problem_t* p, const double* v_sc, const double* beta_sc,
+                         int64_t n_cand, int32_t n_steps, int32_t integrator, double* states_out,
+                         void* ws, size_t ws_bytes, mpc_stream_t stream);
+int mpc_rollout_finalize(const mpc_problem_t* p, const double* v_sc, const double* beta_sc,
+                         int64_t n_cand, int32_t n_steps, int64_t index_base, double incumbent,
+                         int32_t integrator, int32_t with_states, void* ws, size_t ws_bytes,
+                         mpc_result_t* out, mpc_stream_t stream);
+
+/* Batched robots: R problems, robot r owns columns
+ * [r*cand_per_problem, (r+1)*cand_per_problem) of the [n_steps][R*cand] SoA.
+ * problems / incumbents (nullable => +inf) / out are device arrays of R.
+ * Result indices are local to the robot (0 .. cand_per_problem-1). */
+size_t mpc_batched_workspace_bytes(int32_t n_problems, int64_t cand_per_problem, int32_t n_steps);
+int mpc_rollout_argmin_batched(const mpc_problem_t* problems, const double* incumbents,
+                               int32_t n_problems, const double* v_sc, const double* beta_sc,
+                               int64_t cand_per_problem, int32_t n_steps, int32_t integrator,
+                               void* ws, size_t ws_bytes, mpc_result_t* out, mpc_stream_t stream);
+
+/* Multi-GPU exchange, device side: pick the lexicographic (cost, index) min
+ * of n gathered per-rank results (all_gather output) into *out — the
+ * all-reduce(min+index) of SURVEY §8e.  `found` is recomputed against
+ * `incumbent`.  Device pointers. */
+int mpc_select_winner(const mpc_result_t* results, int32_t n, double incumbent,
+                      mpc_result_t* out, mpc_stream_t stream);
+
+/* Synthetic candidate generator.  Candidate with
+ * global index g = index_base + c:
+ *   if const_prefix && g < n_v*n_beta: constant sequence u = (v_grid[g / n_beta],
+ *      beta_grid[g % n_beta]) at every step (the reference's enumeration, :311-317)
+ *   else step s uses grid entry k = splitmix64(seed ^ (s << 40) ^ g) % (n_v*n_beta)
+ * v_grid / beta_grid are device arrays; outputs are written SoA with leading
+ * dimension ld >= n_cand: v_sc[s * ld + c] (ld = R*cand lets one call fill one
+ * robot's columns of the batched layout). */
+int mpc_sample_controls(const double* v_grid, int32_t n_v, const double* beta_grid,
+                        int32_t n_beta, int64_t n_cand, int32_t n_steps, uint64_t seed,
+                        int64_t index_base, int32_t const_prefix, double* v_sc,
+                        double* beta_sc, int64_t ld, mpc_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DIPLOMJOURNEY_AMD_MPC_ROLLOUT_H */

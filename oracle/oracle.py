@@ -1,0 +1,123 @@
+"""ctypes binding of the CPU oracle (oracle/_build/libmpc_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py — never by the product package.  See
+oracle/mpc_oracle.c for what each function restates (file:line citations into
+the reference).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from diplomjourney_amd.abi import MpcProblem, MpcResult, MPC_INTEG_QK21, MpcError
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libmpc_oracle.so")
+
+_lib = None
+
+_D = ctypes.c_double
+_P = ctypes.c_void_p
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.mpc_oracle_qk21.restype = _D
+        L.mpc_oracle_qk21.argtypes = [_D, _D, _D]
+        L.mpc_oracle_step.restype = None
+        L.mpc_oracle_step.argtypes = [ctypes.POINTER(_D)] * 3 + [_D, _D, _D, _D, _D, ctypes.c_int]
+        L.mpc_oracle_cost.restype = _D
+        L.mpc_oracle_cost.argtypes = [_D] * 6
+        L.mpc_oracle_rollout_argmin.restype = ctypes.c_int
+        L.mpc_oracle_rollout_argmin.argtypes = [
+            ctypes.POINTER(MpcProblem), _P, _P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
+            _D, ctypes.c_int32, ctypes.POINTER(MpcResult), _P, _P]
+        L.mpc_oracle_rollout_argmin_batched.restype = ctypes.c_int
+        L.mpc_oracle_rollout_argmin_batched.argtypes = [
+            _P, _P, ctypes.c_int32, _P, _P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _P]
+        L.mpc_oracle_sample_controls.restype = None
+        L.mpc_oracle_sample_controls.argtypes = [
+            _P, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
+            ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, _P, _P, ctypes.c_int64]
+        _lib = L
+    return _lib
+
+
+def _integ(i):
+    if isinstance(i, str):
+        from diplomjourney_amd.abi import INTEGRATORS
+        return INTEGRATORS[i]
+    return int(i)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def qk21(fval, a, b):
+    return lib().mpc_oracle_qk21(fval, a, b)
+
+
+def step(state, v, beta, L, t_a, t_b, integ=MPC_INTEG_QK21):
+    x, y, p = _D(state[0]), _D(state[1]), _D(state[2])
+    lib().mpc_oracle_step(ctypes.byref(x), ctypes.byref(y), ctypes.byref(p),
+                          v, beta, L, t_a, t_b, _integ(integ))
+    return [x.value, y.value, p.value]
+
+
+def cost(x, y, x_t, y_t, x_0, y_0):
+    return lib().mpc_oracle_cost(x, y, x_t, y_t, x_0, y_0)
+
+
+def rollout_argmin(problem, v_sc, beta_sc, index_base=0, incumbent=float("inf"),
+                   integ=MPC_INTEG_QK21, want_costs=False, want_states=False):
+    """v_sc, beta_sc: float64 arrays [n_steps, n_cand].  Returns (MpcResult, costs, states)."""
+    v_sc = np.ascontiguousarray(v_sc, dtype=np.float64)
+    beta_sc = np.ascontiguousarray(beta_sc, dtype=np.float64)
+    n_steps, n_cand = v_sc.shape
+    costs = np.empty(n_cand) if want_costs else None
+    states = np.empty((n_steps, 3, n_cand)) if want_states else None
+    out = MpcResult()
+    st = lib().mpc_oracle_rollout_argmin(ctypes.byref(problem), _ptr(v_sc), _ptr(beta_sc),
+                                         n_cand, n_steps, index_base, incumbent, _integ(integ),
+                                         ctypes.byref(out), _ptr(costs), _ptr(states))
+    if st != 0:
+        raise MpcError(st, "mpc_oracle_rollout_argmin")
+    return out, costs, states
+
+
+def rollout_argmin_batched(problems, v_sc, beta_sc, cand, incumbents=None, integ=MPC_INTEG_QK21):
+    R = len(problems)
+    parr = (MpcProblem * R)(*problems)
+    v_sc = np.ascontiguousarray(v_sc, dtype=np.float64)
+    beta_sc = np.ascontiguousarray(beta_sc, dtype=np.float64)
+    n_steps = v_sc.shape[0]
+    inc = None if incumbents is None else np.ascontiguousarray(incumbents, dtype=np.float64)
+    out = (MpcResult * R)()
+    st = lib().mpc_oracle_rollout_argmin_batched(
+        ctypes.cast(parr, ctypes.c_void_p), _ptr(inc), R, _ptr(v_sc), _ptr(beta_sc), cand,
+        n_steps, _integ(integ), ctypes.cast(out, ctypes.c_void_p))
+    if st != 0:
+        raise MpcError(st, "mpc_oracle_rollout_argmin_batched")
+    return list(out)
+
+
+def sample_controls(v_grid, beta_grid, n_cand, n_steps, seed, index_base=0, const_prefix=True):
+    v_grid = np.ascontiguousarray(v_grid, dtype=np.float64)
+    beta_grid = np.ascontiguousarray(beta_grid, dtype=np.float64)
+    v_sc = np.empty((n_steps, n_cand))
+    b_sc = np.empty((n_steps, n_cand))
+    lib().mpc_oracle_sample_controls(_ptr(v_grid), len(v_grid), _ptr(beta_grid), len(beta_grid),
+                                     n_cand, n_steps, seed, index_base, int(const_prefix),
+                                     _ptr(v_sc), _ptr(b_sc), n_cand)
+    return v_sc, b_sc

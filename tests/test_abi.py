@@ -1,0 +1,101 @@
+"""The C-ABI library: builds, loads, exports every symbol include/mpc_rollout.h
+declares, agrees with the ctypes struct layout, and validates arguments
+before touching the GPU.  CPU only (no compute calls)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from diplomjourney_amd import abi, native
+
+HEADER = native.HEADER
+
+
+def _declared():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return set(re.findall(r"\b(mpc_[a-z_]+)\s*\(", text))
+
+
+@pytest.fixture(scope="module")
+def so():
+    if native.needs_build():
+        native.build()
+    return ctypes.CDLL(native.LIB_PATH)
+
+
+def test_exports_match_header(so):
+    declared = _declared()
+    assert declared == set(native.EXPORTS)
+    for name in declared:
+        assert hasattr(so, name), name
+
+
+def test_binding_loads():
+    L = native.lib()
+    assert b"gfx950" in L.mpc_version()
+    assert L.mpc_strerror(abi.MPC_ERR_WORKSPACE) == b"workspace too small"
+
+
+def test_struct_layout_matches_c(tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "mpc_rollout.h"\n'
+        "int main(void){printf(\"%zu %zu %zu %zu %zu %zu\\n\", sizeof(mpc_problem_t),"
+        " sizeof(mpc_result_t), offsetof(mpc_result_t, index), offsetof(mpc_result_t, found),"
+        " offsetof(mpc_result_t, v), offsetof(mpc_result_t, traj)); return 0;}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), "-o", str(exe), str(src)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    R = abi.MpcResult
+    assert got == [ctypes.sizeof(abi.MpcProblem), ctypes.sizeof(R), R.index.offset,
+                   R.found.offset, R.v.offset, R.traj.offset]
+
+
+def test_workspace_sizes():
+    L = native.lib()
+    assert L.mpc_workspace_bytes(1, 3) == 16
+    assert L.mpc_workspace_bytes(10**7, 12) == 2048 * 16   # capped grid
+    assert L.mpc_batched_workspace_bytes(4, 10_000, 8) == 4 * 40 * 16
+
+
+def test_argument_validation_without_gpu():
+    """Invalid arguments are rejected before any HIP call."""
+    L = native.lib()
+    p = abi.make_problem(0, 0, 0, 2, 3, 0, 0, 0.5, 0.05, 0.1)
+    fake = ctypes.c_void_p(0x1000)
+    args = dict(v=fake, b=fake, n=100, ns=3, base=0, inc=1e300, integ=0, st=None, ws=fake,
+                wsb=1 << 20, out=fake)
+
+    def call(**kw):
+        a = {**args, **kw}
+        return L.mpc_rollout_argmin(ctypes.byref(p), a["v"], a["b"], a["n"], a["ns"], a["base"],
+                                    a["inc"], a["integ"], a["st"], a["ws"], a["wsb"], a["out"],
+                                    None)
+
+    assert call(n=0) == abi.MPC_ERR_ARG
+    assert call(ns=0) == abi.MPC_ERR_ARG
+    assert call(ns=abi.MPC_MAX_STEPS + 1) == abi.MPC_ERR_ARG
+    assert call(v=None) == abi.MPC_ERR_ARG
+    assert call(out=None) == abi.MPC_ERR_ARG
+    assert call(base=-1) == abi.MPC_ERR_ARG
+    assert call(integ=7) == abi.MPC_ERR_UNSUPPORTED
+    assert call(wsb=8) == abi.MPC_ERR_WORKSPACE
+    assert L.mpc_rollout_argmin(None, fake, fake, 10, 3, 0, 1.0, 0, None, fake, 1 << 20, fake,
+                                None) == abi.MPC_ERR_ARG
+    assert L.mpc_select_winner(None, 1, 1.0, fake, None) == abi.MPC_ERR_ARG
+    assert L.mpc_sample_controls(fake, 3, fake, 4, 10, 3, 1, 0, 1, fake, fake, 5,
+                                 None) == abi.MPC_ERR_ARG  # ld < n_cand
+    assert L.mpc_rollout_argmin_batched(fake, None, 0, fake, fake, 10, 3, 0, fake, 1 << 20,
+                                        fake, None) == abi.MPC_ERR_ARG
+
+
+def test_no_cpu_fallback(monkeypatch, tmp_path):
+    """The product binding raises when the HIP library is absent."""
+    monkeypatch.setattr(native, "_lib", None)
+    monkeypatch.setattr(native, "_LIB_OVERRIDE", str(tmp_path / "missing.so"))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        native.lib()

@@ -1,0 +1,111 @@
+"""Multi-rank path on CPU: world_size-2 `gloo` groups run the same sharding +
+exchange code the RCCL path runs (gather_results + lexicographic selection),
+with per-shard results from the oracle, and must pick exactly the candidate
+a single scan over all candidates picks — including ties across the shard
+boundary (lowest global index wins)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _problem():
+    from diplomjourney_amd.abi import make_problem
+    return make_problem(0.0, 0.0, 0.4, 2, 3, 0, 0, 0.5, 0.05, 0.1)
+
+
+def _controls(n_cand, n_steps, dup):
+    from oracle import oracle as O
+    V = [0.3 + 0.005 * i for i in range(11)]
+    B = [(-20 + i) * 0.017453292519943295 for i in range(41)]
+    v, b = O.sample_controls(V, B, n_cand, n_steps, seed=99)
+    if dup:
+        # best candidate duplicated on both sides of the shard boundary
+        _, costs, _ = O.rollout_argmin(_problem(), v, b, want_costs=True)
+        k = int(np.argmin(costs))
+        j = n_cand - 1 - (k % 7) if k < n_cand // 2 else k % 7
+        v[:, j], b[:, j] = v[:, k], b[:, k]
+    return v, b
+
+
+def _worker(rank, world, port, n_cand, n_steps, dup, q):
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from diplomjourney_amd.abi import RESULT_BYTES
+        from diplomjourney_amd.distributed import gather_results, select_winner_host, shard_range
+        from oracle import oracle as O
+        v, b = _controls(n_cand, n_steps, dup)
+        lo, hi = shard_range(n_cand, rank, world)
+        res, _, _ = O.rollout_argmin(_problem(), v[:, lo:hi], b[:, lo:hi], index_base=lo)
+        local = torch.frombuffer(bytearray(bytes(res)), dtype=torch.uint8)
+        assert local.numel() == RESULT_BYTES
+        gathered = gather_results(local)
+        win = select_winner_host(gathered.numpy().tobytes(), incumbent=float(sys.maxsize))
+        q.put((rank, win.index, win.cost, win.found, win.trajectory()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_cand,n_steps,dup", [(4000, 3, False), (3001, 10, True),
+                                                (2000, 12, True)])
+def test_gloo_two_ranks_match_single_scan(n_cand, n_steps, dup):
+    sys.path.insert(0, REPO)
+    from oracle import oracle as O
+    v, b = _controls(n_cand, n_steps, dup)
+    ref, _, _ = O.rollout_argmin(_problem(), v, b, incumbent=float(sys.maxsize))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_cand, n_steps, dup, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, idx, cost, found, traj in outs:
+        assert idx == ref.index and cost == ref.cost and found == ref.found
+        assert traj == ref.trajectory()
+
+
+def test_shard_range_partitions():
+    from diplomjourney_amd.distributed import shard_range
+    for n in (1, 7, 10_000_000, 1_250_001):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(n, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            sizes = [hi - lo for lo, hi in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_select_winner_host_order():
+    from diplomjourney_amd.abi import MpcResult
+    from diplomjourney_amd.distributed import select_winner_host
+
+    def rec(cost, index):
+        r = MpcResult()
+        r.cost, r.index, r.n_steps = cost, index, 3
+        return r
+    recs = [rec(5.0, 700), rec(5.0, 300), rec(float("inf"), -1), rec(6.0, 1)]
+    w = select_winner_host(recs, incumbent=10.0)
+    assert (w.index, w.found) == (300, 1)
+    assert select_winner_host(recs, incumbent=5.0).found == 0      # strict <
+    none = select_winner_host([rec(float("inf"), -1)] * 2)
+    assert (none.index, none.found) == (-1, 0)

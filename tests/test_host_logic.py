@@ -1,0 +1,136 @@
+"""Host-side logic of the drop-in (config, grids, CoordinateTree index
+arithmetic, operator events, cost helper) against the reference's own
+outputs.  CPU only."""
+import math
+
+import pytest
+
+from diplomjourney_amd import config
+from diplomjourney_amd import math_model_tree as mmt
+from diplomjourney_amd.CoordinateTree import CoordinateTree
+
+
+def test_config_matches_reference(units):
+    for name, val in units["config"].items():
+        ours = getattr(config, name)
+        assert ours == val and type(ours) is type(val), name
+
+
+def test_module_constants(units):
+    assert mmt.radius_u_turn == units["consts_mmt"]["radius_u_turn"]
+
+
+def test_first_incumbent(scenario):
+    """optimal_criterion = control_criterion([x_0, y_0, phi_0]) with config's
+    target (math_model_tree.py:676)."""
+    mmt.reset_state()
+    assert mmt.optimal_criterion == scenario["first_incumbent"] == 10000050990.195135
+
+
+def test_grids_bitwise(units):
+    for r in units["grids"]["velocities"]:
+        assert mmt.vector_of_velocities(r["in"]) == r["out"], r["in"]
+    for r in units["grids"]["betas"]:
+        assert mmt.vector_of_beta_angles(r["in"]) == r["out"], r["in"]
+
+
+def test_grids_from_scenario(scenario):
+    """Every call's grid is the reference grid around the previous (v, beta)."""
+    for rec in scenario["calls"][:151]:
+        if rec["call"] == 0:
+            continue
+        prev = scenario["calls"][rec["call"] - 1]["ret"]
+        assert mmt.vector_of_velocities(prev[3]) == rec["V"]
+        assert mmt.vector_of_beta_angles(prev[4]) == rec["B"]
+
+
+def test_is_on_target(units):
+    for r in units["is_on_target"]:
+        assert mmt.is_on_target(*r["in"]) == r["out"]
+
+
+def test_host_cost(units):
+    saved = (mmt.x_t, mmt.y_t, mmt.x_0, mmt.y_0)
+    try:
+        for r in units["costs"]:
+            mmt.x_t, mmt.y_t, mmt.x_0, mmt.y_0 = r["in"][:4]
+            assert mmt.control_criterion(r["in"][4:6] + [0.0]) == r["cost"]
+    finally:
+        mmt.x_t, mmt.y_t, mmt.x_0, mmt.y_0 = saved
+
+
+@pytest.mark.parametrize("entry", range(6))
+def test_coordinate_tree_index(units, entry):
+    t = units["tree"][entry]
+    ct = CoordinateTree(t["S1"], 3, device="cpu")
+    assert ct.get_size() == t["size"]
+    if "parents" in t:
+        got = [ct.get_index_of_parent(j) for j in range(ct.get_size())]
+        assert got == t["parents"]
+    else:
+        assert [ct.get_index_of_parent(j) for j in t["js"]] == t["parents_at"]
+
+
+def test_coordinate_tree_size_451(units):
+    ct = CoordinateTree(451, 3, device="cpu")
+    assert ct.get_size() == units["tree"][-1]["size_formula"] == 91_937_703
+
+
+def test_coordinate_tree_nodes_roundtrip():
+    ct = CoordinateTree(4, 3, device="cpu")
+    assert ct[0] is None and ct[4 + 3] is None          # unwritten slots read None
+    ct[4 + 2] = [1.0, 2.0, 0.5, 0.3, -0.1]               # layer 1, node 2
+    assert ct[6] == [1.0, 2.0, 0.5, 0.3, -0.1]
+    assert ct[4 + 16 + 5] is None                        # layer 2, never-used node
+    with pytest.raises(IndexError):
+        ct[4 + 16 + 5] = [0, 0, 0, 0, 0]
+    ct.clear()
+    assert ct[6] is None
+    assert ct.get_index_of_parent(4 + 16 + 2) == [4 + 2, 2]
+
+
+def test_coordinate_tree_deeper_horizon():
+    ct = CoordinateTree(3, 5, device="cpu")
+    assert ct.get_size() == 3 + 9 + 27 + 81 + 243
+    j = ct.offsets[4] + 1                                 # layer 4, node 1
+    assert ct.get_index_of_parent(j) == [ct.offsets[3] + 1, ct.offsets[2] + 1,
+                                         ct.offsets[1] + 1, 1]
+
+
+def test_operator_events(scenario):
+    """turn_right (p=60), turn_left (p=90), new_target (p=110) targets and
+    the globals they set (math_model_tree.py:118-226, :564-569, :617-624)."""
+    calls = scenario["calls"]
+    for ev in scenario["events"]:
+        ax, ay, aphi, tx, ty, av = ev["args"]
+        ret = calls[ev["after_call"]]["ret"]
+        assert (ax, ay, aphi) == tuple(ret[:3])
+        if ev["p"] == 60:
+            assert mmt._turn_target(ax, ay, aphi, 2, -1) == (tx, ty)
+        elif ev["p"] == 90:
+            assert mmt._turn_target(ax, ay, aphi, 2, +1) == (tx, ty)
+        else:
+            assert (tx, ty) == (2, 3)
+        mmt.reset_state()
+        mmt.x_t, mmt.y_t = ev["pre"]["x_t"], ev["pre"]["y_t"]
+        mmt.new_target(ax, ay, aphi, tx, ty, av)
+        post = ev["post"]
+        assert (mmt.x_t, mmt.y_t, mmt.x_0, mmt.y_0) == (post["x_t"], post["y_t"], post["x_0"],
+                                                         post["y_0"])
+        assert mmt.steps_for_slowing == 10     # slow_down(radians(30)) in new_target
+    mmt.reset_state()
+
+
+def test_slow_down_bands():
+    for deg, want in ((5, 0), (30, 10), (45, 10), (60, 20), (90, 20)):
+        mmt.slow_down(math.radians(deg))
+        assert mmt.steps_for_slowing == want
+    mmt.reset_state()
+
+
+def test_candidate_enumeration_order():
+    """k = a*|B| + b: v outer, beta inner (math_model_tree.py:311-317)."""
+    v_sc, b_sc = mmt.candidate_controls([0.1, 0.2], [-1.0, 0.0, 1.0], 3, "cpu")
+    assert v_sc.shape == (3, 6)
+    assert v_sc[0].tolist() == [0.1, 0.1, 0.1, 0.2, 0.2, 0.2]
+    assert b_sc[2].tolist() == [-1.0, 0.0, 1.0, -1.0, 0.0, 1.0]
