@@ -4,13 +4,15 @@
 // math_model_tree.py in IEEE fp64 with the reference's operation order.  The
 // translation unit is compiled with -ffp-contract=off so each + - * / is one
 // rounding, exactly as in CPython; tan/sincos/sqrt are the ROCm device
-// library's fp64 routines (faithfully rounded, <= 1 ulp from glibc's).
+// kernel's own fp64 routines (mpc_trig.h; faithfully rounded, <= 1 ulp from
+// glibc's).
 #pragma once
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/mpc_rollout.h"
+#include "mpc_trig.h"
 
 namespace mpc {
 
@@ -29,7 +31,7 @@ struct Consts {
 };
 
 // QUADPACK dqk21 Kronrod weights wgk(1..11).
-__device__ constexpr double kWGK[11] = {
+constexpr double kWGK[11] = {
     0.011694638867371874278064396062192, 0.032558162307964727478818972459390,
     0.054755896574351996031381300244580, 0.075039674810919952767043140916190,
     0.093125454583697605535065465083366, 0.109387158802297641899210590325805,
@@ -39,7 +41,7 @@ __device__ constexpr double kWGK[11] = {
 
 // sp.quad(f, t, t+dt) of a constant integrand (math_model_tree.py:91-96).
 template <int INTEG>
-__device__ __forceinline__ double quad_const(double f, const Consts& K) {
+MPC_HD __forceinline__ double quad_const(double f, const Consts& K) {
   if constexpr (INTEG == MPC_INTEG_RECT) {
     return f * K.h;
   } else {
@@ -56,19 +58,19 @@ __device__ __forceinline__ double quad_const(double f, const Consts& K) {
 // iteration_of_predict (math_model_tree.py:111-115): heading first, then
 // position with the updated heading (semi-implicit bicycle step).
 template <int INTEG>
-__device__ __forceinline__ void step(double& x, double& y, double& ph, double v, double beta,
-                                     const Consts& K) {
+MPC_HD __forceinline__ void step(double& x, double& y, double& ph, double v, double beta,
+                                 const Consts& K) {
   const double w = K.L_pow2 ? v * K.inv_L : v / K.L;          // _velocity / L   (:78)
-  const double dphi = quad_const<INTEG>(w * tan(beta), K);     // angle_phi       (:107)
+  const double dphi = quad_const<INTEG>(w * trig::tan_fast(beta), K);  // angle_phi (:107)
   ph = ph + dphi;                                              // phi + _phi      (:113)
   double s, c;
-  sincos(ph, &s, &c);
+  trig::sincos_fast(ph, &s, &c);
   x = x + quad_const<INTEG>(v * c, K);                         // coordinate_x    (:99)
   y = y + quad_const<INTEG>(v * s, K);                         // coordinate_y    (:103)
 }
 
 // control_criterion (math_model_tree.py:82-87) on the layer-N state.
-__device__ __forceinline__ double cost(double x, double y, const Consts& K) {
+MPC_HD __forceinline__ double cost(double x, double y, const Consts& K) {
   const double ex = K.x_t - x, ey = K.y_t - y;
   const double dist_target = sqrt(ex * ex + ey * ey);          // :66
   double d;

@@ -31,6 +31,18 @@ namespace mpc {
 namespace {
 
 constexpr int kBlock = 256;           // 4 waves of 64
+// Build-time tuning knobs (A/B-tested with tools/probe_gpu.py variants):
+#ifndef MPC_CPL
+#define MPC_CPL 2            // candidates per lane on the aligned path (2 or 4)
+#endif
+#ifndef MPC_UNROLL_STEPS
+#define MPC_UNROLL_STEPS 0   // 1: fully unroll compile-time horizons
+#endif
+#ifndef MPC_MIN_WAVES
+#define MPC_MIN_WAVES 1      // __launch_bounds__ minimum waves per SIMD
+#endif
+constexpr int kCplWide = MPC_CPL;
+static_assert(kCplWide == 2 || kCplWide == 4, "MPC_CPL must be 2 or 4");
 constexpr int kWaves = kBlock / 64;
 constexpr int64_t kMaxBlocks = 2048;  // 256 CUs x 8 resident blocks upper bound
 constexpr int kFinBlock = 1024;
@@ -77,19 +89,25 @@ __device__ __forceinline__ void rollout_lane(const Consts& K, const double* __re
     y[j] = K.y;
     ph[j] = K.phi;
   }
-  auto body = [&](int sr) {
-    double vv[CPL], bb[CPL];
-    if constexpr (CPL == 2) {
-      const double2 v2 = *reinterpret_cast<const double2*>(v + sr * ld + c0);
-      const double2 b2 = *reinterpret_cast<const double2*>(b + sr * ld + c0);
-      vv[0] = v2.x;
-      vv[1] = v2.y;
-      bb[0] = b2.x;
-      bb[1] = b2.y;
+  // Controls of step sr for this lane's CPL candidates: 16 B per lane per
+  // array on the wide path (one 1 KiB wave-instruction each).
+  auto load = [&](int sr, double (&vv)[CPL], double (&bb)[CPL]) {
+    if constexpr (CPL >= 2) {
+#pragma unroll
+      for (int h = 0; h < CPL; h += 2) {
+        const double2 v2 = *reinterpret_cast<const double2*>(v + sr * ld + c0 + h);
+        const double2 b2 = *reinterpret_cast<const double2*>(b + sr * ld + c0 + h);
+        vv[h] = v2.x;
+        vv[h + 1] = v2.y;
+        bb[h] = b2.x;
+        bb[h + 1] = b2.y;
+      }
     } else {
       vv[0] = v[sr * ld + c0];
       bb[0] = b[sr * ld + c0];
     }
+  };
+  auto body = [&](int sr, const double (&vv)[CPL], const double (&bb)[CPL]) {
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
       step<INTEG>(x[j], y[j], ph[j], vv[j], bb[j], K);
@@ -100,18 +118,38 @@ __device__ __forceinline__ void rollout_lane(const Consts& K, const double* __re
       }
     }
   };
-  if constexpr (NS > 0) {
+  double va[CPL], ba[CPL], vb[CPL], bb_[CPL];
+  load(0, va, ba);
+  if constexpr (NS > 0 && MPC_UNROLL_STEPS) {
 #pragma unroll
-    for (int s = 0; s < NS; ++s) body(s);
+    for (int s = 0; s < NS; s += 2) {
+      if (s + 1 < NS) load(s + 1, vb, bb_);
+      body(s, va, ba);
+      if (s + 1 < NS) {
+        if (s + 2 < NS) load(s + 2, va, ba);
+        body(s + 1, vb, bb_);
+      }
+    }
   } else {
-    for (int s = 0; s < n_steps; ++s) body(s);
+    const int ns = NS > 0 ? NS : n_steps;
+    // Software pipeline, two steps per trip (ping-pong registers, no copies):
+    // the next step's controls are in flight while this step's trig chain runs.
+#pragma unroll 1
+    for (int s = 0; s < ns; s += 2) {
+      if (s + 1 < ns) load(s + 1, vb, bb_);
+      body(s, va, ba);
+      if (s + 1 < ns) {
+        if (s + 2 < ns) load(s + 2, va, ba);
+        body(s + 1, vb, bb_);
+      }
+    }
   }
 #pragma unroll
   for (int j = 0; j < CPL; ++j) cst[j] = cost(x[j], y[j], K);
 }
 
 template <int NS, int CPL, int INTEG, bool STATES>
-__global__ __launch_bounds__(kBlock) void k_rollout_argmin(Consts K, const double* __restrict__ v,
+__global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(Consts K, const double* __restrict__ v,
                                                            const double* __restrict__ b,
                                                            int64_t n_cand, int n_steps,
                                                            int64_t n_tiles, Rec* __restrict__ part,
@@ -120,7 +158,7 @@ __global__ __launch_bounds__(kBlock) void k_rollout_argmin(Consts K, const doubl
   int64_t best_i = INT64_MAX;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     const int64_t c0 = tile * (kBlock * CPL) + threadIdx.x * CPL;
-    if (c0 < n_cand) {  // CPL == 2 requires even n_cand, so c0+1 < n_cand too
+    if (c0 < n_cand) {  // CPL > 1 requires n_cand % CPL == 0: the whole group is valid
       double cst[CPL];
       rollout_lane<NS, CPL, INTEG, STATES>(K, v, b, n_cand, c0, n_steps, cst, states, n_cand);
 #pragma unroll
@@ -228,7 +266,7 @@ __device__ __forceinline__ Consts consts_from_problem(const mpc_problem_t& p) {
 }
 
 template <int NS, int CPL, int INTEG>
-__global__ __launch_bounds__(kBlock) void k_rollout_argmin_batched(
+__global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin_batched(
     const mpc_problem_t* __restrict__ probs, const double* __restrict__ v,
     const double* __restrict__ b, int64_t cand, int n_steps, int64_t ld, Rec* __restrict__ part) {
   const int r = blockIdx.y;
@@ -419,10 +457,14 @@ size_t mpc_workspace_bytes(int64_t n_cand, int32_t n_steps) {
 }
 
 // Number of block records phase 1 writes (phase 2 must agree).
+static bool wide_ok(const double* v_sc, const double* beta_sc, int64_t n) {
+  return (n % kCplWide == 0) && aligned16(v_sc) && aligned16(beta_sc);
+}
+
 static int64_t partial_count(const double* v_sc, const double* beta_sc, int64_t n_cand,
                              bool with_states) {
-  const bool pair = !with_states && (n_cand % 2 == 0) && aligned16(v_sc) && aligned16(beta_sc);
-  const int64_t tiles = cdiv(n_cand, kBlock * (pair ? 2 : 1));
+  const bool wide = !with_states && wide_ok(v_sc, beta_sc, n_cand);
+  const int64_t tiles = cdiv(n_cand, kBlock * (wide ? kCplWide : 1));
   return std::min<int64_t>(tiles, kMaxBlocks);
 }
 
@@ -456,11 +498,11 @@ int mpc_rollout_partials(const mpc_problem_t* p, const double* v_sc, const doubl
       k_rollout_argmin<0, 1, MPC_INTEG_QK21, true>
           <<<grid, kBlock, 0, st>>>(K, v_sc, beta_sc, n_cand, n_steps, tiles, part, states_out);
   } else {
-    const bool pair = (n_cand % 2 == 0) && aligned16(v_sc) && aligned16(beta_sc);
-    const int64_t tiles = cdiv(n_cand, kBlock * (pair ? 2 : 1));
-    if (pair) {
-      if (rect) launch_by_steps<2, MPC_INTEG_RECT>(grid, st, K, v_sc, beta_sc, n_cand, n_steps, tiles, part);
-      else launch_by_steps<2, MPC_INTEG_QK21>(grid, st, K, v_sc, beta_sc, n_cand, n_steps, tiles, part);
+    const bool wide = wide_ok(v_sc, beta_sc, n_cand);
+    const int64_t tiles = cdiv(n_cand, kBlock * (wide ? kCplWide : 1));
+    if (wide) {
+      if (rect) launch_by_steps<kCplWide, MPC_INTEG_RECT>(grid, st, K, v_sc, beta_sc, n_cand, n_steps, tiles, part);
+      else launch_by_steps<kCplWide, MPC_INTEG_QK21>(grid, st, K, v_sc, beta_sc, n_cand, n_steps, tiles, part);
     } else {
       if (rect) launch_by_steps<1, MPC_INTEG_RECT>(grid, st, K, v_sc, beta_sc, n_cand, n_steps, tiles, part);
       else launch_by_steps<1, MPC_INTEG_QK21>(grid, st, K, v_sc, beta_sc, n_cand, n_steps, tiles, part);
@@ -520,16 +562,17 @@ int mpc_rollout_argmin_batched(const mpc_problem_t* problems, const double* incu
     return MPC_ERR_WORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t ld = static_cast<int64_t>(n_problems) * cand_per_problem;
-  const bool pair = (cand_per_problem % 2 == 0) && aligned16(v_sc) && aligned16(beta_sc);
-  const int cpl = pair ? 2 : 1;
+  const bool pair = wide_ok(v_sc, beta_sc, cand_per_problem) &&
+                    (static_cast<int64_t>(n_problems) * cand_per_problem) % kCplWide == 0;
+  const int cpl = pair ? kCplWide : 1;
   const int64_t tiles = cdiv(cand_per_problem, kBlock * cpl);
   const int64_t per_robot = std::min<int64_t>(tiles, rollout_blocks(cand_per_problem));
   const dim3 grid(static_cast<unsigned>(per_robot), static_cast<unsigned>(n_problems));
   Rec* part = static_cast<Rec*>(ws);
   const bool rect = integrator == MPC_INTEG_RECT;
   if (pair) {
-    if (rect) launch_batched_by_steps<2, MPC_INTEG_RECT>(grid, st, problems, v_sc, beta_sc, cand_per_problem, n_steps, ld, part);
-    else launch_batched_by_steps<2, MPC_INTEG_QK21>(grid, st, problems, v_sc, beta_sc, cand_per_problem, n_steps, ld, part);
+    if (rect) launch_batched_by_steps<kCplWide, MPC_INTEG_RECT>(grid, st, problems, v_sc, beta_sc, cand_per_problem, n_steps, ld, part);
+    else launch_batched_by_steps<kCplWide, MPC_INTEG_QK21>(grid, st, problems, v_sc, beta_sc, cand_per_problem, n_steps, ld, part);
   } else {
     if (rect) launch_batched_by_steps<1, MPC_INTEG_RECT>(grid, st, problems, v_sc, beta_sc, cand_per_problem, n_steps, ld, part);
     else launch_batched_by_steps<1, MPC_INTEG_QK21>(grid, st, problems, v_sc, beta_sc, cand_per_problem, n_steps, ld, part);

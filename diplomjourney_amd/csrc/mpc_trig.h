@@ -1,0 +1,175 @@
+// mpc_trig.h — fp64 tan and sincos for the MPC step, written for gfx950's VALU.
+//
+// Why not the device library's tan(): on gfx950 it evaluates the Payne-Hanek
+// large-argument reduction unconditionally (both reductions are computed and
+// one is selected), ~70 of its ~155 instructions per call, although the
+// kernel's arguments are steering angles (|beta| <= 1.05) and headings.
+// Here the reduction is a branch-free 3-part Cody-Waite (pi/2 = P1+P2+P3, P1
+// and P2 with 33 significant bits, so k*P1 and k*P2 are exact for |k| <= 2^19)
+// producing a double-double remainder, followed by near-minimax polynomials on
+// |r| <= pi/4 (coefficients from tools/fit_trig.py, mpmath).  Arguments beyond
+// the Cody-Waite range take a (wave-divergent, in practice never taken) branch
+// to the library routine, so results are correct for every input.
+//
+// Accuracy: faithful (< 1 ulp); see tests/test_trig.py for the measured error
+// against mpmath and the agreement rate with glibc (which the reference uses).
+// The same source compiles for the host, where it is tested bit for bit
+// against the device build.
+#pragma once
+
+#include <math.h>
+
+#if defined(__HIPCC__)
+#define MPC_HD __host__ __device__
+#else
+#define MPC_HD
+#endif
+
+namespace mpc {
+namespace trig {
+
+// Cody-Waite pi/2 = P1 + P2 + P3 (tools/fit_trig.py)
+constexpr double kP1 = 0x1.921fb54400000p+0;
+constexpr double kP2 = 0x1.0b4611a600000p-34;
+constexpr double kP3 = 0x1.3198a2e037073p-69;
+constexpr double kTwoOverPi = 0x1.45f306dc9c883p-1;
+// |x| <= kFastMax  =>  |k| <= 2^19
+constexpr double kFastMax = 0x1p19 * 1.5707963267948966;
+
+// sin(r) = r + r^3 * S(r^2);  S[6] = -1/6          (highest degree first)
+constexpr double kS[7] = {-0x1.ab17d393166dcp-41, 0x1.61217f0abf087p-33, -0x1.ae645412c46d3p-26,
+                          0x1.71de3a5460952p-19,  -0x1.a01a01a019938p-13, 0x1.1111111111110p-7,
+                          -0x1.5555555555555p-3};
+// cos(r) = 1 - r^2/2 + r^4 * C(r^2);  C[6] = 1/24
+constexpr double kC[7] = {0x1.ab785a9b7d08fp-45,  -0x1.9394ba0c2b394p-37, 0x1.1eed8deb973d2p-29,
+                          -0x1.27e4fb7712d61p-22, 0x1.a01a01a019d0ap-16,  -0x1.6c16c16c16c16p-10,
+                          0x1.5555555555555p-5};
+// tan(r) = r + r^3 * T(r^2);  T[15] = 1/3
+constexpr double kT[16] = {0x1.090dd50c4e26cp-18, -0x1.46ffa51d98a1ep-17, 0x1.47c7055045e77p-16,
+                           -0x1.562bc1c9b4034p-17, 0x1.c6cf3cb6be147p-16, 0x1.1c9d930b42224p-15,
+                           0x1.9e442bd4b147bp-14,  0x1.f4827710891adp-13, 0x1.35639727a6c93p-11,
+                           0x1.7da2a66dc0210p-10,  0x1.d6d3d9596ac82p-9,  0x1.226e353ec9951p-7,
+                           0x1.664f48834f976p-6,   0x1.ba1ba1ba1a515p-5,  0x1.111111111111bp-3,
+                           0x1.5555555555555p-2};
+
+// fma(a, b, c) with c a compile-time coefficient.  On gfx950 hipcc selects
+// the two-address v_fmac_f64 for a Horner step and then has to copy the
+// (loop-invariant) coefficient into the accumulator first: two VALU ops and
+// two VGPRs per coefficient.  The three-address VOP3 form with the
+// coefficient in an SGPR pair is one VALU op and no VGPRs.
+MPC_HD inline double fma_k(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+#else
+  return fma(a, b, c);
+#endif
+}
+
+template <int N>
+MPC_HD inline double horner(const double (&c)[N], double z, int skip_last = 0) {
+  double p = c[0];
+#pragma unroll
+  for (int i = 1; i < N; ++i)
+    if (i < N - skip_last) p = fma_k(p, z, c[i]);
+  return p;
+}
+
+// x = k*pi/2 + (hi + lo), |hi| <= pi/4 (+ulps); exact-ish double-double.
+struct Reduced {
+  double hi, lo;
+  int q;
+};
+
+MPC_HD inline Reduced reduce_pio2(double x) {
+  // + 0.0 turns rint's -0 into +0, so x = -0 reduces to hi = -0 (sin(-0) = -0)
+  const double k = rint(x * kTwoOverPi) + 0.0;
+  double r = fma(-k, kP1, x);  // exact: k*P1 exact, x and k*P1 within a factor 2
+  double w = k * kP2;          // exact
+  const double t = r;
+  r = t - w;
+  w = fma(k, kP3, -((t - r) - w));
+  Reduced o;
+  o.hi = r - w;
+  o.lo = (r - o.hi) - w;
+  o.q = static_cast<int>(k);
+  return o;
+}
+
+// sin / cos of hi + lo, |hi| <= pi/4
+MPC_HD inline double ksin(double x, double y) {
+  const double z = x * x;
+  const double v = z * x;
+  const double r = horner(kS, z, 1);  // S1 + z*(S2 + ...)
+  return x - ((z * (0.5 * y - v * r) - y) - v * kS[6]);
+}
+
+MPC_HD inline double kcos(double x, double y) {
+  const double z = x * x;
+  const double r = z * horner(kC, z);
+  const double hz = 0.5 * z;
+  const double w = 1.0 - hz;
+  return w + (((1.0 - w) - hz) + (z * r - x * y));
+}
+
+// 1/d for |d| in [2^-60, 2]: hardware reciprocal estimate + two Newton steps
+// (relative error ~2^-100 before the final rounding).
+MPC_HD inline double recip(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r = __builtin_amdgcn_rcp(d);
+#else
+  double r = 1.0 / d;
+#endif
+  r = fma(r, fma(-d, r, 1.0), r);
+  r = fma(r, fma(-d, r, 1.0), r);
+  return r;
+}
+
+// tan (odd == 0) or -1/tan (odd == 1) of hi + lo, |hi| <= pi/4.  Branch-free:
+// both quadrant forms are formed and one is selected per lane.
+MPC_HD inline double ktan(double x, double y, bool odd) {
+  const double z = x * x;
+  const double u = (x * z) * horner(kT, z);
+  const double th = x + u;
+  double tl = (x - th) + u;               // exact error of th (|x| >= |u|)
+  tl = fma(y, fma(th, th, 1.0), tl);      // + lo * sec^2
+  const double a = -recip(th);            // -1/th
+  const double e = fma(a, th, 1.0) + a * tl;  // 1 + a*(th + tl)
+  const double cot = fma(a, e, a);
+  return odd ? cot : th + tl;
+}
+
+// MPC_TRIG_NO_FALLBACK: instruction-count builds only (tools), drops the
+// large-argument branch.
+MPC_HD inline double tan_fast(double x) {
+#ifndef MPC_TRIG_NO_FALLBACK
+  if (!(fabs(x) <= kFastMax)) return ::tan(x);  // huge or NaN
+#endif
+  const Reduced r = reduce_pio2(x);
+  const double t = ktan(r.hi, r.lo, (r.q & 1) != 0);
+  return x == 0.0 ? x : t;  // tan(+-0) = +-0
+}
+
+MPC_HD inline void sincos_fast(double x, double* s, double* c) {
+#ifndef MPC_TRIG_NO_FALLBACK
+  if (!(fabs(x) <= kFastMax)) {
+    *s = ::sin(x);
+    *c = ::cos(x);
+    return;
+  }
+#endif
+  const Reduced r = reduce_pio2(x);
+  const double sn = ksin(r.hi, r.lo);
+  const double cs = kcos(r.hi, r.lo);
+  const int q = r.q & 3;
+  double S = (q & 1) ? cs : sn;
+  double C = (q & 1) ? sn : cs;
+  if (q & 2) S = -S;
+  if ((q + 1) & 2) C = -C;
+  *s = S;
+  *c = C;
+}
+
+}  // namespace trig
+}  // namespace mpc

@@ -1,0 +1,74 @@
+"""The kernel's arithmetic, built for the host (tests/replica_harness.cpp),
+against the oracle (CPU) and against the GPU (bitwise).
+
+* CPU: replica vs oracle — identical arg-min on reference-shaped inputs,
+  states within a few ulp (the only difference is tan/sin/cos: device
+  routines vs glibc, and x*x vs glibc pow(x, 2) in the cost).
+* GPU: the kernel's states (CoordinateTree output) and its winner's cost are
+  the replica's BIT FOR BIT — the device code does exactly the IEEE
+  operations it was written to do.
+"""
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import call_controls, call_problem
+from harness import replica_rollout
+
+INC_MAX = float(sys.maxsize)
+
+
+def _case(n, ns, seed):
+    from oracle import oracle as O
+    from diplomjourney_amd import math_model_tree as mmt
+    V = mmt.vector_of_velocities(0.5)
+    B = mmt.vector_of_beta_angles(0.0)
+    return O.sample_controls(V, B, n, ns, seed)
+
+
+def test_replica_vs_oracle_scenario(scenario, oracle):
+    for rec in scenario["calls"][::7]:
+        v, b = call_controls(rec)
+        for integ in ("qk21", "rect"):
+            st, costs = replica_rollout(call_problem(rec), v, b, integ)
+            ref, rc, rs = oracle.rollout_argmin(call_problem(rec), v, b, integ=integ,
+                                                want_costs=True, want_states=True)
+            assert int(np.argmin(costs)) == ref.index
+            assert np.abs(st - rs).max() <= 1e-15
+            assert np.allclose(costs, rc, rtol=1e-14, atol=0)
+
+
+def test_replica_vs_oracle_synthetic(oracle):
+    from diplomjourney_amd.abi import make_problem
+    v, b = _case(20_000, 10, 5)
+    p = make_problem(0.2, -0.1, 2.9, 2, 3, 0.5, 0.5, 0.5, 0.35, 0.4)
+    st, costs = replica_rollout(p, v, b, "rect")
+    ref, rc, rs = oracle.rollout_argmin(p, v, b, integ="rect", want_costs=True, want_states=True)
+    assert int(np.argmin(costs)) == ref.index
+    assert np.abs(st - rs).max() <= 1e-14
+    frac_equal = np.mean(st == rs)
+    assert frac_equal > 0.5                 # most states bit-identical to the reference math
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,ns,integ", [(100_000, 5, "rect"), (30_001, 12, "qk21"),
+                                        (4096, 32, "rect")])
+def test_gpu_bitwise_equals_replica(engine, n, ns, integ):
+    from diplomjourney_amd.abi import make_problem
+    v, b = _case(n, ns, 11)
+    p = make_problem(-1.0, 0.5, -2.2, 2, 3, 0.25, -0.5, 0.5, 7.45, 7.5)
+    st, costs = replica_rollout(p, v, b, integ)
+    vd = torch.as_tensor(v, device="cuda")
+    bd = torch.as_tensor(b, device="cuda")
+    states = torch.empty((ns, 3, n), dtype=torch.float64, device="cuda")
+    engine.rollout_argmin(p, vd, bd, incumbent=INC_MAX, integrator=integ, states=states)
+    got = engine.fetch()
+    assert np.array_equal(states.cpu().numpy(), st)
+    k = int(np.argmin(costs))
+    assert got.index == k and got.cost == costs[k]
+    engine.rollout_argmin(p, vd, bd, incumbent=INC_MAX, integrator=integ)   # streaming path
+    fast = engine.fetch()
+    assert fast.index == k and fast.cost == costs[k]
+    assert fast.trajectory() == [list(st[s, :, k]) for s in range(ns)]

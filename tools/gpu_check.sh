@@ -7,8 +7,8 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 python -m pytest tests -x -q -m gpu > $OUT/pytest_gpu.log 2>&1 && \
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
-timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --cpu-seconds 0 --steps 30 > $OUT/bench_prof.json 2> $OUT/prof.err
+timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --cpu-seconds 0 --steps 30 > $OUT/bench_prof.json 2> $OUT/prof.err
 rc=$?
 echo "rc=$rc"
 tail -3 $OUT/pytest_gpu.log; cat $OUT/smoke.log; cat $OUT/bench.json

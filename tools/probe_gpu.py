@@ -98,7 +98,13 @@ def time_kernel(eng, n_cand, n_steps, integ, reps=20, odd=False):
 def main():
     quick = "--quick" in sys.argv
     eng = Expansion("cuda:0")
-    emit(check="device", name=torch.cuda.get_device_name(0))
+    emit(check="device", name=torch.cuda.get_device_name(0),
+         lib=os.environ.get("DIPLOMJOURNEY_MPC_LIB", "in-tree"))
+    if "--time-only" in sys.argv:
+        for n_steps, integ in ((10, "rect"), (10, "qk21"), (3, "rect"), (12, "rect")):
+            time_kernel(eng, 1_000_000, n_steps, integ)
+        time_kernel(eng, 8_000_000, 10, "rect")
+        return
     for n_steps, integ in ((10, "rect"), (10, "qk21"), (3, "rect"), (12, "rect"), (11, "rect"), (8, "rect")):
         time_kernel(eng, 1_000_000, n_steps, integ)
     time_kernel(eng, 1_000_000, 10, "rect", odd=True)
