@@ -12,7 +12,7 @@
 //                      (bitwise the same arithmetic as the rollout lane).
 //   k_rollout_argmin_batched / k_finalize_batched   robot-segmented variant.
 //   k_select_winner    lexicographic min over gathered per-rank results.
-//   k_sample_controls  synthetic control sequences (splitmix64 over the grid).
+//   k_sample_controls  synthetic control sequences (splitmix64 -> grid entry).
 //
 // HBM traffic of k_rollout_argmin: 16 B per candidate-step read once
 // (v, beta fp64 SoA), 16 B per block written.  See DESIGN.md for the roofline.
@@ -175,12 +175,61 @@ __global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(Consts
   if (threadIdx.x == 0) part[blockIdx.x] = Rec{best_k, best_i};
 }
 
-// Re-roll one candidate (the winner) and fill the result record.
+// Re-roll the winner and fill the result record.  Called by ALL threads of
+// the block once thread 0 holds the winner (key, col).  The N-step recurrence
+// is split so that only additions stay serial: lane s computes the state-free
+// heading increment dphi_s = Q((v_s/L) tan(beta_s)); lane 0 accumulates the
+// headings phi_s = phi_{s-1} + dphi_s; lane s evaluates sincos(phi_s) and the
+// two position increments; lane 0 accumulates x and y.  Every operation and
+// every accumulation order is that of step<INTEG>(), so the emitted states
+// are bitwise those the arg-min scored, at ~3N dependent adds of latency
+// instead of N dependent trig chains.
 template <int INTEG>
 __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
-                            const double* __restrict__ b, int64_t ld, int64_t col, int n_steps,
-                            uint64_t key, int64_t reported_index, double incumbent,
+                            const double* __restrict__ b, int64_t ld, int n_steps, uint64_t key,
+                            int64_t col, int64_t reported_index, double incumbent,
                             mpc_result_t* __restrict__ out) {
+  __shared__ double s_dphi[MPC_MAX_STEPS], s_phi[MPC_MAX_STEPS];
+  __shared__ double s_dx[MPC_MAX_STEPS], s_dy[MPC_MAX_STEPS], s_v0, s_b0;
+  __shared__ uint64_t s_key;
+  __shared__ int64_t s_col, s_rep;
+  if (threadIdx.x == 0) {
+    s_key = key;
+    s_col = col;
+    s_rep = reported_index;
+  }
+  __syncthreads();
+  key = s_key;
+  col = s_col;
+  const int lane = threadIdx.x;
+  double vs = 0.0;
+  if (key != ~0ull && lane < n_steps) {
+    vs = v[lane * ld + col];
+    const double bs = b[lane * ld + col];
+    if (lane == 0) {
+      s_v0 = vs;
+      s_b0 = bs;
+    }
+    const double w = K.L_pow2 ? vs * K.inv_L : vs / K.L;
+    s_dphi[lane] = quad_const<INTEG>(w * trig::tan_fast(bs), K);
+  }
+  __syncthreads();
+  if (lane == 0 && key != ~0ull) {
+    double ph = K.phi;
+    for (int st = 0; st < n_steps; ++st) {
+      ph = ph + s_dphi[st];
+      s_phi[st] = ph;
+    }
+  }
+  __syncthreads();
+  if (key != ~0ull && lane < n_steps) {
+    double sn, cs;
+    trig::sincos_fast(s_phi[lane], &sn, &cs);
+    s_dx[lane] = quad_const<INTEG>(vs * cs, K);
+    s_dy[lane] = quad_const<INTEG>(vs * sn, K);
+  }
+  __syncthreads();
+  if (lane != 0) return;
   out->n_steps = n_steps;
   if (key == ~0ull) {
     out->cost = __builtin_inf();
@@ -192,16 +241,17 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
   }
   const double c = key_cost(key);
   out->cost = c;
-  out->index = reported_index;
+  out->index = s_rep;
   out->found = c < incumbent ? 1 : 0;
-  out->v = v[col];
-  out->beta = b[col];
-  double x = K.x, y = K.y, ph = K.phi;
-  for (int s = 0; s < n_steps; ++s) {
-    step<INTEG>(x, y, ph, v[s * ld + col], b[s * ld + col], K);
-    out->traj[s][0] = x;
-    out->traj[s][1] = y;
-    out->traj[s][2] = ph;
+  out->v = s_v0;
+  out->beta = s_b0;
+  double x = K.x, y = K.y;
+  for (int st = 0; st < n_steps; ++st) {
+    x = x + s_dx[st];
+    y = y + s_dy[st];
+    out->traj[st][0] = x;
+    out->traj[st][1] = y;
+    out->traj[st][2] = s_phi[st];
   }
 }
 
@@ -233,8 +283,8 @@ __global__ __launch_bounds__(kFinBlock) void k_finalize(const Rec* __restrict__ 
         k = s_key[w];
         i = s_idx[w];
       }
-    emit_winner<INTEG>(K, v, b, n_cand, i, n_steps, k, index_base + i, incumbent, out);
   }
+  emit_winner<INTEG>(K, v, b, n_cand, n_steps, k, i, index_base + i, incumbent, out);
 }
 
 // --------------------------- batched robots --------------------------------
@@ -310,11 +360,9 @@ __global__ __launch_bounds__(kBlock) void k_finalize_batched(
     }
   }
   block_argmin(k, i);
-  if (threadIdx.x == 0) {
-    const Consts K = consts_from_problem(probs[r]);
-    const double inc = incumbents ? incumbents[r] : __builtin_inf();
-    emit_winner<INTEG>(K, v, b, ld, r * cand + i, n_steps, k, i, inc, &out[r]);
-  }
+  const Consts K = consts_from_problem(probs[r]);
+  const double inc = incumbents ? incumbents[r] : __builtin_inf();
+  emit_winner<INTEG>(K, v, b, ld, n_steps, k, r * cand + i, i, inc, &out[r]);
 }
 
 // --------------------------- exchange + sampler ----------------------------
@@ -337,21 +385,55 @@ __global__ void k_select_winner(const mpc_result_t* __restrict__ res, int n, dou
   out->found = (bk != ~0ull && out->cost < incumbent) ? 1 : 0;
 }
 
+// Grid entry of one (step, candidate): candidate g < n_grid of the constant
+// prefix is the reference's enumeration k = g; otherwise the top 32 bits of
+// splitmix64(seed ^ s<<40 ^ g) are mapped onto [0, n_grid) by multiply-shift
+// (Lemire's fastrange: no integer division on the VALU).
+__device__ __forceinline__ uint32_t grid_entry(uint64_t seed, int s, uint64_t g, uint32_t n_grid,
+                                               int cprefix) {
+  if (cprefix && g < n_grid) return static_cast<uint32_t>(g);
+  const uint64_t h = splitmix64(seed ^ (static_cast<uint64_t>(s) << 40) ^ g);
+  return static_cast<uint32_t>(((h >> 32) * static_cast<uint64_t>(n_grid)) >> 32);
+}
+
+constexpr int kSampleLdsEntries = 2048;  // expanded (v, beta) grid staged in LDS
+
+// One thread per candidate pair (16-B stores), looping over the steps.  The
+// grid |V| x |B| (<= 451 entries for the reference's acceleration limits) is
+// expanded once per block into LDS, so the per-element lookup is one
+// ds_read_b128 instead of a division by |B| and two global loads.
 __global__ __launch_bounds__(kBlock) void k_sample_controls(
     const double* __restrict__ vg, int nv, const double* __restrict__ bg, int nb, int64_t n_cand,
     int n_steps, uint64_t seed, int64_t base, int cprefix, double* __restrict__ v,
-    double* __restrict__ b, int64_t ld) {
-  const uint64_t n_grid = static_cast<uint64_t>(nv) * static_cast<uint64_t>(nb);
-  const int64_t total = n_cand * n_steps;
-  for (int64_t e = blockIdx.x * static_cast<int64_t>(kBlock) + threadIdx.x; e < total;
-       e += static_cast<int64_t>(gridDim.x) * kBlock) {
-    const int64_t s = e / n_cand, c = e - s * n_cand;
+    double* __restrict__ b, int64_t ld, int pairs) {
+  __shared__ double2 s_grid[kSampleLdsEntries];
+  const uint32_t n_grid = static_cast<uint32_t>(nv) * static_cast<uint32_t>(nb);
+  const bool in_lds = n_grid <= kSampleLdsEntries;
+  if (in_lds) {
+    for (uint32_t k = threadIdx.x; k < n_grid; k += kBlock)
+      s_grid[k] = make_double2(vg[k / nb], bg[k % nb]);
+    __syncthreads();
+  }
+  auto lookup = [&](uint32_t k) -> double2 {
+    return in_lds ? s_grid[k] : make_double2(vg[k / nb], bg[k % nb]);
+  };
+  const int cpt = pairs ? 2 : 1;
+  const int64_t n_items = n_cand / cpt;
+  for (int64_t it = blockIdx.x * static_cast<int64_t>(kBlock) + threadIdx.x; it < n_items;
+       it += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const int64_t c = it * cpt;
     const uint64_t g = static_cast<uint64_t>(base + c);
-    const uint64_t k = (cprefix && g < n_grid)
-                           ? g
-                           : splitmix64(seed ^ (static_cast<uint64_t>(s) << 40) ^ g) % n_grid;
-    v[s * ld + c] = vg[k / static_cast<uint64_t>(nb)];
-    b[s * ld + c] = bg[k % static_cast<uint64_t>(nb)];
+    for (int st = 0; st < n_steps; ++st) {
+      const double2 e0 = lookup(grid_entry(seed, st, g, n_grid, cprefix));
+      if (pairs) {
+        const double2 e1 = lookup(grid_entry(seed, st, g + 1, n_grid, cprefix));
+        *reinterpret_cast<double2*>(v + st * ld + c) = make_double2(e0.x, e1.x);
+        *reinterpret_cast<double2*>(b + st * ld + c) = make_double2(e0.y, e1.y);
+      } else {
+        v[st * ld + c] = e0.x;
+        b[st * ld + c] = e0.y;
+      }
+    }
   }
 }
 
@@ -603,11 +685,13 @@ int mpc_sample_controls(const double* v_grid, int32_t n_v, const double* beta_gr
   if (!v_grid || !beta_grid || !v_sc || !beta_sc || n_v < 1 || n_beta < 1 || n_cand < 1 ||
       n_steps < 1 || index_base < 0 || ld < n_cand)
     return MPC_ERR_ARG;
-  const int64_t total = n_cand * n_steps;
-  const int64_t grid = std::min<int64_t>(cdiv(total, kBlock), 8192);
+  if (static_cast<int64_t>(n_v) * n_beta > 0xFFFFFFFFll) return MPC_ERR_ARG;
+  const int pairs = (n_cand % 2 == 0) && (ld % 2 == 0) && aligned16(v_sc) && aligned16(beta_sc);
+  const int64_t items = pairs ? n_cand / 2 : n_cand;
+  const int64_t grid = std::min<int64_t>(cdiv(items, kBlock), 4096);
   k_sample_controls<<<grid, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
       v_grid, n_v, beta_grid, n_beta, n_cand, n_steps, seed, index_base, const_prefix, v_sc,
-      beta_sc, ld);
+      beta_sc, ld, pairs);
   return last_hip_status();
 }
 

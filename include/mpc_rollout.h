@@ -123,7 +123,8 @@ int mpc_select_winner(const mpc_result_t* results, int32_t n, double incumbent,
  * global index g = index_base + c:
  *   if const_prefix && g < n_v*n_beta: constant sequence u = (v_grid[g / n_beta],
  *      beta_grid[g % n_beta]) at every step (the reference's enumeration, :311-317)
- *   else step s uses grid entry k = splitmix64(seed ^ (s << 40) ^ g) % (n_v*n_beta)
+ *   else step s uses grid entry k = (hi32(splitmix64(seed ^ (s << 40) ^ g)) * n) >> 32
+ *      with n = n_v*n_beta (multiply-shift map of the hash onto [0, n))
  * v_grid / beta_grid are device arrays; outputs are written SoA with leading
  * dimension ld >= n_cand: v_sc[s * ld + c] (ld = R*cand lets one call fill one
  * robot's columns of the batched layout). */
