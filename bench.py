@@ -57,6 +57,15 @@ def parse():
     ap.add_argument("--integrator", default="rect", choices=["rect", "qk21"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="per-core time budget of the cpu_baseline sample (0 = skip)")
+    ap.add_argument("--host-loop", action="store_true",
+                    help="drive the episode from the host (one 808-B read + host update per "
+                         "step) instead of the device-resident episode")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse N ranks on fewer GPUs (exchange staged via host)")
+    ap.add_argument("--candidates-per-gpu", type=int, default=None,
+                    help="override the workload's per-GPU candidate count")
+    ap.add_argument("--dump-log", default=None,
+                    help="write the device episode's per-step log (rank 0) to this JSON file")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per launch for the roofline 'traffic' field")
     return ap.parse_args()
@@ -94,31 +103,43 @@ def main():
 
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    dev_index = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     group = None
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
     from diplomjourney_amd.expansion import Expansion
     eng = Expansion(device)
 
     if args.workload == "E":
         return bench_robots(args, wl, eng, rank, world, cpu)
 
-    from diplomjourney_amd.episode import Episode, percentile
-    n_total = wl["per_gpu"] * world
-    ep = Episode(eng, n_total, wl["n_steps"], rank=rank, world=world,
-                 integrator=args.integrator, group=group)
+    from diplomjourney_amd.episode import DeviceEpisode, Episode, percentile
+    n_total = (args.candidates_per_gpu or wl["per_gpu"]) * world
+    if args.host_loop:
+        ep = Episode(eng, n_total, wl["n_steps"], rank=rank, world=world,
+                     integrator=args.integrator, group=group)
+    else:
+        ep = DeviceEpisode(eng, n_total, wl["n_steps"], rank=rank, world=world,
+                           integrator=args.integrator, group=group,
+                           log_capacity=args.steps + args.warmup)
     for _ in range(args.warmup):
         ep.step()
-    ep.kernel_ms.clear()
-    ep.step_ms.clear()
+    Ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    kern = [(Ev(), Ev()) for _ in range(args.steps)]
+    marks = [Ev() for _ in range(args.steps + 1)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ep.step(time_kernel=True)
+    for i in range(args.steps):
+        marks[i].record()
+        ep.step(events=kern[i])
+    marks[-1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -127,10 +148,20 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kern_ms = sum(ep.kernel_ms) / len(ep.kernel_ms)
+    kern_ms = sum(a.elapsed_time(b) for a, b in kern) / len(kern)
+    step_gpu_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)]
     bytes_launch = 16.0 * wl["n_steps"] * ep.n_local
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     value = n_total * args.steps / elapsed
+    if not args.host_loop:
+        log = ep.read_log()
+        assert len(log) == args.steps + args.warmup and all(r.index >= 0 for r in log)
+        episodes = log[-1].episode
+        if args.dump_log and rank == 0:
+            with open(args.dump_log, "w") as fh:
+                json.dump([{f: getattr(r, f) for f, _ in r._fields_} for r in log], fh)
+    else:
+        episodes = ep.episodes
     out = {
         "metric": METRIC, "value": value, "unit": "rollouts/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -138,10 +169,12 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": wl["desc"], "n_steps": wl["n_steps"],
                    "candidates_per_gpu": ep.n_local, "candidates_total": n_total,
-                   "integrator": args.integrator, "episodes_started": ep.episodes,
+                   "integrator": args.integrator, "episodes_started": episodes,
+                   "episode_loop": "host" if args.host_loop else "device-resident",
                    "parallelism": f"candidate-sharded x{world}" + (", all_gather(808 B)/step"
                                                                    if world > 1 else "")},
-        "p50_ms": percentile(ep.step_ms, 50), "p90_ms": percentile(ep.step_ms, 90),
+        "p50_ms": percentile(step_gpu_ms, 50), "p90_ms": percentile(step_gpu_ms, 90),
+        "p50_note": "GPU time per MPC step (HIP events between step starts)",
         "kernel_ms": kern_ms,
         "roofline": roofline(achieved, bytes_launch, args.traffic_json),
         "cpu_baseline": cpu,

@@ -55,7 +55,26 @@ class MpcResult(ctypes.Structure):
                 "traj": self.trajectory()}
 
 
+class MpcEpisodeConfig(ctypes.Structure):
+    """mpc_episode_config_t: the device-resident math_mpc loop's constants."""
+    _fields_ = [(n, ctypes.c_double) for n in (
+        "start_x", "start_y", "start_phi", "start_v", "start_beta", "target_x", "target_y",
+        "L", "delta_t", "eps", "v_max", "v_min", "delta_v", "ratio_v", "delta_beta",
+        "ratio_beta", "beta_bound", "radius_u_turn", "turn_distance", "event_target_x",
+        "event_target_y")] + [(n, ctypes.c_int32) for n in (
+        "p_turn_right", "p_turn_left", "p_new_target", "slow_new_target", "slow_turn",
+        "max_steps")] + [("seed", ctypes.c_uint64)]
+
+
+class MpcEpisodeLog(ctypes.Structure):
+    """mpc_episode_log_t: one MPC step of the device-resident episode."""
+    _fields_ = [("step", ctypes.c_int64), ("index", ctypes.c_int64), ("p", ctypes.c_int32),
+                ("episode", ctypes.c_int32)] + [(n, ctypes.c_double) for n in (
+                    "cost", "x", "y", "phi", "v", "beta")]
+
+
 RESULT_BYTES = ctypes.sizeof(MpcResult)
+LOG_BYTES = ctypes.sizeof(MpcEpisodeLog)
 PROBLEM_BYTES = ctypes.sizeof(MpcProblem)
 
 STATUS_TEXT = {

@@ -148,12 +148,14 @@ __device__ __forceinline__ void rollout_lane(const Consts& K, const double* __re
   for (int j = 0; j < CPL; ++j) cst[j] = cost(x[j], y[j], K);
 }
 
-template <int NS, int CPL, int INTEG, bool STATES>
-__global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(Consts K, const double* __restrict__ v,
-                                                           const double* __restrict__ b,
-                                                           int64_t n_cand, int n_steps,
-                                                           int64_t n_tiles, Rec* __restrict__ part,
-                                                           double* __restrict__ states) {
+// KDEV: the problem constants come from device memory (the device-resident
+// episode writes them; no host round-trip) instead of the kernel arguments.
+template <int NS, int CPL, int INTEG, bool STATES, bool KDEV = false>
+__global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(
+    Consts Karg, const Consts* __restrict__ Kdev, const double* __restrict__ v,
+    const double* __restrict__ b, int64_t n_cand, int n_steps, int64_t n_tiles,
+    Rec* __restrict__ part, double* __restrict__ states) {
+  const Consts K = KDEV ? *Kdev : Karg;
   uint64_t best_k = ~0ull;
   int64_t best_i = INT64_MAX;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
@@ -255,13 +257,23 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
   }
 }
 
-template <int INTEG>
-__global__ __launch_bounds__(kFinBlock) void k_finalize(const Rec* __restrict__ part, int n_part,
-                                                        Consts K, const double* __restrict__ v,
-                                                        const double* __restrict__ b,
-                                                        int64_t n_cand, int n_steps,
-                                                        int64_t index_base, double incumbent,
-                                                        mpc_result_t* __restrict__ out) {
+struct EpisodeState;
+struct EpisodeHook {           // single-GPU episode: finalize also advances it
+  EpisodeState* S;             // nullptr: no hook
+  mpc_episode_log_t* log;
+  int cap;
+};
+__device__ void episode_hook(const mpc_episode_config_t& c, const EpisodeHook& h,
+                             const mpc_result_t& r);
+
+template <int INTEG, bool KDEV = false>
+__global__ __launch_bounds__(kFinBlock) void k_finalize(
+    const Rec* __restrict__ part, int n_part, Consts Karg, const Consts* __restrict__ Kdev,
+    const double* __restrict__ v, const double* __restrict__ b, int64_t n_cand, int n_steps,
+    int64_t index_base, double incumbent_arg, const double* __restrict__ incumbent_dev,
+    mpc_result_t* __restrict__ out, mpc_episode_config_t ecfg = {}, EpisodeHook hook = {}) {
+  const Consts K = KDEV ? *Kdev : Karg;
+  const double incumbent = KDEV ? *incumbent_dev : incumbent_arg;
   __shared__ uint64_t s_key[kFinBlock / 64];
   __shared__ int64_t s_idx[kFinBlock / 64];
   uint64_t k = ~0ull;
@@ -285,6 +297,7 @@ __global__ __launch_bounds__(kFinBlock) void k_finalize(const Rec* __restrict__ 
       }
   }
   emit_winner<INTEG>(K, v, b, n_cand, n_steps, k, i, index_base + i, incumbent, out);
+  if (KDEV && hook.S && threadIdx.x == 0) episode_hook(ecfg, hook, *out);
 }
 
 // --------------------------- batched robots --------------------------------
@@ -401,21 +414,13 @@ constexpr int kSampleLdsEntries = 2048;  // expanded (v, beta) grid staged in LD
 // One thread per candidate pair (16-B stores), looping over the steps.  The
 // grid |V| x |B| (<= 451 entries for the reference's acceleration limits) is
 // expanded once per block into LDS, so the per-element lookup is one
-// ds_read_b128 instead of a division by |B| and two global loads.
-__global__ __launch_bounds__(kBlock) void k_sample_controls(
-    const double* __restrict__ vg, int nv, const double* __restrict__ bg, int nb, int64_t n_cand,
-    int n_steps, uint64_t seed, int64_t base, int cprefix, double* __restrict__ v,
-    double* __restrict__ b, int64_t ld, int pairs) {
-  __shared__ double2 s_grid[kSampleLdsEntries];
-  const uint32_t n_grid = static_cast<uint32_t>(nv) * static_cast<uint32_t>(nb);
-  const bool in_lds = n_grid <= kSampleLdsEntries;
-  if (in_lds) {
-    for (uint32_t k = threadIdx.x; k < n_grid; k += kBlock)
-      s_grid[k] = make_double2(vg[k / nb], bg[k % nb]);
-    __syncthreads();
-  }
+// ds_read_b128 instead of a division by |B| and two loads.
+__device__ void sample_items(const double2* s_grid, const double* vg, int nb, uint32_t n_grid,
+                             int64_t n_cand, int n_steps, uint64_t seed, int64_t base,
+                             int cprefix, double* __restrict__ v, double* __restrict__ b,
+                             int64_t ld, int pairs) {
   auto lookup = [&](uint32_t k) -> double2 {
-    return in_lds ? s_grid[k] : make_double2(vg[k / nb], bg[k % nb]);
+    return s_grid ? s_grid[k] : make_double2(vg[k / nb], 0.0);
   };
   const int cpt = pairs ? 2 : 1;
   const int64_t n_items = n_cand / cpt;
@@ -435,6 +440,302 @@ __global__ __launch_bounds__(kBlock) void k_sample_controls(
       }
     }
   }
+}
+
+__global__ __launch_bounds__(kBlock) void k_sample_controls(
+    const double* __restrict__ vg, int nv, const double* __restrict__ bg, int nb, int64_t n_cand,
+    int n_steps, uint64_t seed, int64_t base, int cprefix, double* __restrict__ v,
+    double* __restrict__ b, int64_t ld, int pairs) {
+  __shared__ double2 s_grid[kSampleLdsEntries];
+  const uint32_t n_grid = static_cast<uint32_t>(nv) * static_cast<uint32_t>(nb);
+  if (n_grid > kSampleLdsEntries) {
+    // large grids: direct lookups (one division per element)
+    const int cpt = pairs ? 2 : 1;
+    for (int64_t it = blockIdx.x * static_cast<int64_t>(kBlock) + threadIdx.x; it < n_cand / cpt;
+         it += static_cast<int64_t>(gridDim.x) * kBlock) {
+      const int64_t c = it * cpt;
+      for (int st = 0; st < n_steps; ++st)
+        for (int j = 0; j < cpt; ++j) {
+          const uint32_t k = grid_entry(seed, st, base + c + j, n_grid, cprefix);
+          v[st * ld + c + j] = vg[k / nb];
+          b[st * ld + c + j] = bg[k % nb];
+        }
+    }
+    return;
+  }
+  for (uint32_t k = threadIdx.x; k < n_grid; k += kBlock)
+    s_grid[k] = make_double2(vg[k / nb], bg[k % nb]);
+  __syncthreads();
+  sample_items(s_grid, vg, nb, n_grid, n_cand, n_steps, seed, base, cprefix, v, b, ld, pairs);
+}
+
+// --------------------------- device-resident episode -----------------------
+constexpr int kEpMaxGrid = 64;
+
+struct EpisodeState {
+  Consts K;            // this step's problem constants (k_episode_prepare)
+  double incumbent;    // optimal_criterion at the start of this step
+  double x, y, phi, v, beta;
+  double x_t, y_t, x_0, y_0;
+  double t;
+  uint64_t seed;       // this step's sampler seed
+  int64_t step;
+  int32_t p, m, steps_for_slowing, episodes;
+  int32_t nv, nb;
+  double grid_v[kEpMaxGrid];
+  double grid_b[kEpMaxGrid];
+};
+
+__device__ Consts episode_consts(const EpisodeState& S, double x, double y, double phi, double L,
+                                 double t_a, double t_b) {
+  mpc_problem_t p;
+  p.x = x;
+  p.y = y;
+  p.phi = phi;
+  p.x_t = S.x_t;
+  p.y_t = S.y_t;
+  p.x_0 = S.x_0;
+  p.y_0 = S.y_0;
+  p.L = L;
+  p.t_a = t_a;
+  p.t_b = t_b;
+  return consts_from_problem(p);
+}
+
+// Episode.reset() / math_mpc's prologue (:521-541): start pose, target, line
+// origin at the start, t = 0, p = 1, m = 0, incumbent = control_criterion of
+// the origin (the reference's first optimal_criterion, :676).
+__device__ void episode_restart(const mpc_episode_config_t& c, EpisodeState& S) {
+  S.x = c.start_x;
+  S.y = c.start_y;
+  S.phi = c.start_phi;
+  S.v = c.start_v;
+  S.beta = c.start_beta;
+  S.x_t = c.target_x;
+  S.y_t = c.target_y;
+  S.x_0 = c.start_x;
+  S.y_0 = c.start_y;
+  S.t = 0.0;
+  S.p = 1;
+  S.m = 0;
+  S.steps_for_slowing = 0;
+  S.episodes += 1;
+  const Consts K0 = episode_consts(S, S.x_0, S.y_0, 0.0, c.L, 0.0, c.delta_t);
+  S.incumbent = cost(S.x_0, S.y_0, K0);
+}
+
+__global__ void k_episode_reset(mpc_episode_config_t c, EpisodeState* __restrict__ S) {
+  if (threadIdx.x != 0) return;
+  S->step = 0;
+  S->episodes = 0;
+  episode_restart(c, *S);
+}
+
+// Grids (:239-256) with the reference's expressions and the slow-down
+// override (:312-316), computed by one wave: lane i evaluates grid point i,
+// a ballot compacts the accepted points in order.  Writes s_v[nv], s_b[nb].
+__device__ void episode_grids(const mpc_episode_config_t& c, const EpisodeState& S,
+                              double* s_v, double* s_b, int& nv_out, int& nb_out) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int n_v = 1 + 2 * static_cast<int>(c.ratio_v);
+  int nv = 0;
+  double vmin = __builtin_inf();
+  for (int base = 0; base < n_v; base += 64) {
+    const int i = base + lane;
+    const double cand = S.v + c.delta_v * (static_cast<double>(i) - c.ratio_v);
+    const bool ok = i < n_v && !(cand < 0.0) && cand < c.v_max;
+    const uint64_t m = __ballot(ok);
+    const int pos = nv + __popcll(m & below);
+    if (ok && pos < kEpMaxGrid) s_v[pos] = cand;
+    double mn = ok ? cand : __builtin_inf();
+    for (int off = 32; off > 0; off >>= 1) mn = fmin(mn, __shfl_xor(mn, off, 64));
+    vmin = fmin(vmin, mn);
+    nv += __popcll(m);
+  }
+  nv = nv < kEpMaxGrid ? nv : kEpMaxGrid;
+  if (S.steps_for_slowing > 0 && nv > 0) {
+    const double vel = vmin > c.v_min ? vmin : c.v_min;
+    for (int i = lane; i < nv; i += 64) s_v[i] = vel;
+  }
+  const int n_b = 1 + 2 * static_cast<int>(c.ratio_beta);
+  int nb = 0;
+  for (int base = 0; base < n_b; base += 64) {
+    const int i = base + lane;
+    const double cand = S.beta + c.delta_beta * (static_cast<double>(i) - c.ratio_beta);
+    const bool ok = i < n_b && fabs(cand) <= c.beta_bound;
+    const uint64_t m = __ballot(ok);
+    const int pos = nb + __popcll(m & below);
+    if (ok && pos < kEpMaxGrid) s_b[pos] = cand;
+    nb += __popcll(m);
+  }
+  nv_out = nv;
+  nb_out = nb < kEpMaxGrid ? nb : kEpMaxGrid;
+}
+
+__device__ __forceinline__ uint64_t episode_seed(const mpc_episode_config_t& c,
+                                                 const EpisodeState& S) {
+  return c.seed + 0x9E3779B9ull * static_cast<uint64_t>(S.p + 1000 * S.episodes);
+}
+
+// _turn_target (math_model_tree.py:142-215 sectors; sign = +1 left, -1 right).
+__device__ void turn_target(double ax, double ay, double aphi, double d, double R, double sign,
+                            double& tx, double& ty) {
+  const double pi = 3.141592653589793;
+  double sn, cs;
+  if (pi / 2 <= aphi && aphi <= 3 * pi / 2) {
+    if (aphi <= pi) {
+      trig::sincos_fast(aphi - pi / 2, &sn, &cs);
+      tx = ax - sign * d * cs - R * sn;
+      ty = ay - sign * d * sn + R * cs;
+    } else {
+      trig::sincos_fast(aphi - pi, &sn, &cs);
+      tx = ax + sign * d * sn - R * cs;
+      ty = ay - sign * d * cs - R * sn;
+    }
+  } else if (aphi <= 2 * pi) {
+    trig::sincos_fast(aphi - 3 * pi / 2, &sn, &cs);
+    tx = ax + sign * d * cs + R * sn;
+    ty = ay + sign * d * sn - R * cs;
+  } else {
+    trig::sincos_fast(aphi, &sn, &cs);
+    tx = ax - sign * d * sn + R * cs;
+    ty = ay + sign * d * cs + R * sn;
+  }
+}
+
+// Episode._advance: finishing logic (:392-414), events (:564-569), restart.
+__device__ void episode_advance(const mpc_episode_config_t& c, EpisodeState* __restrict__ S,
+                                const mpc_result_t& r, mpc_episode_log_t* __restrict__ log,
+                                int cap) {
+  S->steps_for_slowing -= 1;
+  S->incumbent = 9223372036854775808.0;  // float(sys.maxsize), :428
+  if (log && cap > 0) {
+    mpc_episode_log_t& L = log[S->step % cap];
+    L.step = S->step;
+    L.index = r.found ? r.index : -1;
+    L.p = S->p;
+    L.episode = S->episodes;
+    L.cost = r.cost;
+  }
+  S->step += 1;
+  if (r.found) {
+    const int last = r.n_steps - 1;
+    const int probe = last < 2 ? last : 2;
+    int k = 0;
+    if (S->m == 2) {
+      k = 2;
+    } else if (S->m == 1) {
+      k = 1;
+      S->m += 1;
+    } else {
+      const double ex = S->x_t - r.traj[probe][0], ey = S->y_t - r.traj[probe][1];
+      if (ex * ex + ey * ey <= c.eps) S->m += 1;
+    }
+    k = k < last ? k : last;
+    S->x = r.traj[k][0];
+    S->y = r.traj[k][1];
+    S->phi = r.traj[k][2];
+    S->v = r.v;
+    S->beta = r.beta;
+    double tx, ty;
+    if (S->p == c.p_turn_right) {
+      turn_target(S->x, S->y, S->phi, c.turn_distance, c.radius_u_turn, -1.0, tx, ty);
+      S->x_t = tx; S->y_t = ty; S->x_0 = S->x; S->y_0 = S->y;
+      S->steps_for_slowing = c.slow_turn;
+    }
+    if (S->p == c.p_turn_left) {
+      turn_target(S->x, S->y, S->phi, c.turn_distance, c.radius_u_turn, +1.0, tx, ty);
+      S->x_t = tx; S->y_t = ty; S->x_0 = S->x; S->y_0 = S->y;
+      S->steps_for_slowing = c.slow_turn;
+    }
+    if (S->p == c.p_new_target) {
+      S->x_t = c.event_target_x; S->y_t = c.event_target_y; S->x_0 = S->x; S->y_0 = S->y;
+      S->steps_for_slowing = c.slow_new_target;
+    }
+    S->p += 1;
+    const double ex = S->x_t - S->x, ey = S->y_t - S->y;
+    if (ex * ex + ey * ey <= c.eps || S->p > c.max_steps) episode_restart(c, *S);
+  }
+  if (log && cap > 0) {
+    mpc_episode_log_t& L = log[(S->step - 1) % cap];
+    L.x = S->x;
+    L.y = S->y;
+    L.phi = S->phi;
+    L.v = S->v;
+    L.beta = S->beta;
+  }
+}
+
+
+__device__ void episode_hook(const mpc_episode_config_t& c, const EpisodeHook& h,
+                             const mpc_result_t& r) {
+  episode_advance(c, h.S, r, h.log, h.cap);
+}
+
+// Multi-GPU: lexicographic (cost, global index) selection over the gathered
+// per-rank winners (the all-reduce(min+index)), then the episode update.
+__global__ void k_episode_advance(mpc_episode_config_t c, EpisodeState* __restrict__ S,
+                                  const mpc_result_t* __restrict__ res, int n,
+                                  mpc_episode_log_t* __restrict__ log, int cap) {
+  if (threadIdx.x != 0) return;
+  int best = 0;
+  uint64_t bk = ~0ull;
+  int64_t bi = INT64_MAX;
+  for (int r = 0; r < n; ++r) {
+    const uint64_t k = res[r].index < 0 ? ~0ull : cost_key(res[r].cost);
+    const int64_t i = res[r].index < 0 ? INT64_MAX : res[r].index;
+    if (r == 0 || rec_less(k, i, bk, bi)) {
+      best = r;
+      bk = k;
+      bi = i;
+    }
+  }
+  mpc_result_t w = res[best];
+  w.found = (bk != ~0ull && w.cost < S->incumbent) ? 1 : 0;
+  episode_advance(c, S, w, log, cap);
+}
+
+// Device-resident episode, sampler + step prologue in one launch: every block
+// derives this step's grid (one wave, ballot compaction) into LDS and samples
+// its candidates; block 0 also publishes t += dt, the problem constants and
+// the seed for the rollout/finalize launches that follow on the stream.
+__global__ __launch_bounds__(kBlock) void k_episode_sample(
+    mpc_episode_config_t c, EpisodeState* __restrict__ S, int64_t n_cand, int n_steps,
+    int64_t base, double* __restrict__ v, double* __restrict__ b, int pairs) {
+  __shared__ double s_v[kEpMaxGrid], s_b[kEpMaxGrid];
+  __shared__ double2 s_grid[kSampleLdsEntries];
+  __shared__ int s_nv, s_nb;
+  if (threadIdx.x < 64) {
+    int nv, nb;
+    episode_grids(c, *S, s_v, s_b, nv, nb);
+    if (threadIdx.x == 0) {
+      s_nv = nv;
+      s_nb = nb;
+    }
+  }
+  __syncthreads();
+  const int nv = s_nv, nb = s_nb;
+  const uint64_t seed = episode_seed(c, *S);
+  const uint32_t n_grid = static_cast<uint32_t>(nv) * static_cast<uint32_t>(nb);
+  const bool in_lds = n_grid <= kSampleLdsEntries;
+  if (in_lds)
+    for (uint32_t k = threadIdx.x; k < n_grid; k += kBlock)
+      s_grid[k] = make_double2(s_v[k / nb], s_b[k % nb]);
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const double t = S->t + c.delta_t;                                      // :302
+    S->K = episode_consts(*S, S->x, S->y, S->phi, c.L, t, t + c.delta_t);
+    S->t = t;
+    S->seed = seed;
+    S->nv = nv;
+    S->nb = nb;
+    for (int i = 0; i < nv; ++i) S->grid_v[i] = s_v[i];
+    for (int i = 0; i < nb; ++i) S->grid_b[i] = s_b[i];
+  }
+  if (n_grid == 0) return;
+  sample_items(in_lds ? s_grid : nullptr, s_v, nb, n_grid, n_cand, n_steps, seed, base, 1, v, b,
+               n_cand, pairs);
 }
 
 // ------------------------------- host side ---------------------------------
@@ -475,22 +776,23 @@ inline int64_t rollout_blocks(int64_t n_cand) {
   return std::max<int64_t>(1, std::min<int64_t>(cdiv(n_cand, kBlock), kMaxBlocks));
 }
 
-template <int NS, int CPL, int INTEG>
-void launch_fixed(dim3 grid, hipStream_t st, const Consts& K, const double* v, const double* b,
-                  int64_t n_cand, int n_steps, int64_t tiles, Rec* part) {
-  k_rollout_argmin<NS, CPL, INTEG, false>
-      <<<grid, kBlock, 0, st>>>(K, v, b, n_cand, n_steps, tiles, part, nullptr);
+template <int NS, int CPL, int INTEG, bool KDEV>
+void launch_fixed(dim3 grid, hipStream_t st, const Consts& K, const Consts* Kdev, const double* v,
+                  const double* b, int64_t n_cand, int n_steps, int64_t tiles, Rec* part) {
+  k_rollout_argmin<NS, CPL, INTEG, false, KDEV>
+      <<<grid, kBlock, 0, st>>>(K, Kdev, v, b, n_cand, n_steps, tiles, part, nullptr);
 }
 
-template <int CPL, int INTEG>
+template <int CPL, int INTEG, bool KDEV = false>
 void launch_by_steps(dim3 grid, hipStream_t st, const Consts& K, const double* v, const double* b,
-                     int64_t n_cand, int n_steps, int64_t tiles, Rec* part) {
+                     int64_t n_cand, int n_steps, int64_t tiles, Rec* part,
+                     const Consts* Kdev = nullptr) {
   switch (n_steps) {
-    case 3: launch_fixed<3, CPL, INTEG>(grid, st, K, v, b, n_cand, n_steps, tiles, part); break;
-    case 8: launch_fixed<8, CPL, INTEG>(grid, st, K, v, b, n_cand, n_steps, tiles, part); break;
-    case 10: launch_fixed<10, CPL, INTEG>(grid, st, K, v, b, n_cand, n_steps, tiles, part); break;
-    case 12: launch_fixed<12, CPL, INTEG>(grid, st, K, v, b, n_cand, n_steps, tiles, part); break;
-    default: launch_fixed<0, CPL, INTEG>(grid, st, K, v, b, n_cand, n_steps, tiles, part); break;
+    case 3: launch_fixed<3, CPL, INTEG, KDEV>(grid, st, K, Kdev, v, b, n_cand, n_steps, tiles, part); break;
+    case 8: launch_fixed<8, CPL, INTEG, KDEV>(grid, st, K, Kdev, v, b, n_cand, n_steps, tiles, part); break;
+    case 10: launch_fixed<10, CPL, INTEG, KDEV>(grid, st, K, Kdev, v, b, n_cand, n_steps, tiles, part); break;
+    case 12: launch_fixed<12, CPL, INTEG, KDEV>(grid, st, K, Kdev, v, b, n_cand, n_steps, tiles, part); break;
+    default: launch_fixed<0, CPL, INTEG, KDEV>(grid, st, K, Kdev, v, b, n_cand, n_steps, tiles, part); break;
   }
 }
 
@@ -575,10 +877,10 @@ int mpc_rollout_partials(const mpc_problem_t* p, const double* v_sc, const doubl
     const int64_t tiles = cdiv(n_cand, kBlock);
     if (rect)
       k_rollout_argmin<0, 1, MPC_INTEG_RECT, true>
-          <<<grid, kBlock, 0, st>>>(K, v_sc, beta_sc, n_cand, n_steps, tiles, part, states_out);
+          <<<grid, kBlock, 0, st>>>(K, nullptr, v_sc, beta_sc, n_cand, n_steps, tiles, part, states_out);
     else
       k_rollout_argmin<0, 1, MPC_INTEG_QK21, true>
-          <<<grid, kBlock, 0, st>>>(K, v_sc, beta_sc, n_cand, n_steps, tiles, part, states_out);
+          <<<grid, kBlock, 0, st>>>(K, nullptr, v_sc, beta_sc, n_cand, n_steps, tiles, part, states_out);
   } else {
     const bool wide = wide_ok(v_sc, beta_sc, n_cand);
     const int64_t tiles = cdiv(n_cand, kBlock * (wide ? kCplWide : 1));
@@ -605,11 +907,13 @@ int mpc_rollout_finalize(const mpc_problem_t* p, const double* v_sc, const doubl
   const Rec* part = static_cast<const Rec*>(ws);
   const int n_part = static_cast<int>(partial_count(v_sc, beta_sc, n_cand, with_states != 0));
   if (integrator == MPC_INTEG_RECT)
-    k_finalize<MPC_INTEG_RECT><<<1, kFinBlock, 0, st>>>(part, n_part, K, v_sc, beta_sc, n_cand,
-                                                        n_steps, index_base, incumbent, out);
+    k_finalize<MPC_INTEG_RECT><<<1, kFinBlock, 0, st>>>(part, n_part, K, nullptr, v_sc, beta_sc,
+                                                        n_cand, n_steps, index_base, incumbent,
+                                                        nullptr, out);
   else
-    k_finalize<MPC_INTEG_QK21><<<1, kFinBlock, 0, st>>>(part, n_part, K, v_sc, beta_sc, n_cand,
-                                                        n_steps, index_base, incumbent, out);
+    k_finalize<MPC_INTEG_QK21><<<1, kFinBlock, 0, st>>>(part, n_part, K, nullptr, v_sc, beta_sc,
+                                                        n_cand, n_steps, index_base, incumbent,
+                                                        nullptr, out);
   return last_hip_status();
 }
 
@@ -692,6 +996,131 @@ int mpc_sample_controls(const double* v_grid, int32_t n_v, const double* beta_gr
   k_sample_controls<<<grid, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
       v_grid, n_v, beta_grid, n_beta, n_cand, n_steps, seed, index_base, const_prefix, v_sc,
       beta_sc, ld, pairs);
+  return last_hip_status();
+}
+
+
+size_t mpc_episode_state_bytes(void) { return sizeof(EpisodeState); }
+
+static int check_episode_cfg(const mpc_episode_config_t* c) {
+  if (!c) return MPC_ERR_ARG;
+  if (!(c->ratio_v >= 0) || !(c->ratio_beta >= 0) || 1 + 2 * static_cast<int>(c->ratio_v) > 4 * kEpMaxGrid ||
+      1 + 2 * static_cast<int>(c->ratio_beta) > 4 * kEpMaxGrid || c->max_steps < 1 || !(c->delta_t > 0))
+    return MPC_ERR_ARG;
+  return MPC_OK;
+}
+
+int mpc_episode_reset(const mpc_episode_config_t* cfg, void* state, mpc_stream_t stream) {
+  if (check_episode_cfg(cfg) != MPC_OK || !state) return MPC_ERR_ARG;
+  k_episode_reset<<<1, 64, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+      *cfg, static_cast<EpisodeState*>(state));
+  return last_hip_status();
+}
+
+static int check_expand_args(const mpc_episode_config_t* cfg, void* state, double* v_sc,
+                             double* beta_sc, int64_t n_cand, int32_t n_steps, int64_t index_base,
+                             int32_t integrator, void* ws, size_t ws_bytes) {
+  if (check_episode_cfg(cfg) != MPC_OK || !state || !v_sc || !beta_sc || n_cand < 1 ||
+      n_steps < 1 || n_steps > MPC_MAX_STEPS || index_base < 0)
+    return MPC_ERR_ARG;
+  if (integrator != MPC_INTEG_QK21 && integrator != MPC_INTEG_RECT) return MPC_ERR_UNSUPPORTED;
+  if (!ws || ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
+  return MPC_OK;
+}
+
+int mpc_episode_sample(const mpc_episode_config_t* cfg, void* state, double* v_sc,
+                       double* beta_sc, int64_t n_cand, int32_t n_steps, int64_t index_base,
+                       mpc_stream_t stream) {
+  if (check_episode_cfg(cfg) != MPC_OK || !state || !v_sc || !beta_sc || n_cand < 1 ||
+      n_steps < 1 || n_steps > MPC_MAX_STEPS || index_base < 0)
+    return MPC_ERR_ARG;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  EpisodeState* S = static_cast<EpisodeState*>(state);
+  const int pairs = (n_cand % 2 == 0) && aligned16(v_sc) && aligned16(beta_sc);
+  const int64_t items = pairs ? n_cand / 2 : n_cand;
+  k_episode_sample<<<std::min<int64_t>(cdiv(items, kBlock), 4096), kBlock, 0, st>>>(
+      *cfg, S, n_cand, n_steps, index_base, v_sc, beta_sc, pairs);
+  return last_hip_status();
+}
+
+int mpc_episode_partials(void* state, const double* v_sc, const double* beta_sc, int64_t n_cand,
+                         int32_t n_steps, int32_t integrator, void* ws, size_t ws_bytes,
+                         mpc_stream_t stream) {
+  if (!state || !v_sc || !beta_sc || n_cand < 1 || n_steps < 1 || n_steps > MPC_MAX_STEPS)
+    return MPC_ERR_ARG;
+  if (integrator != MPC_INTEG_QK21 && integrator != MPC_INTEG_RECT) return MPC_ERR_UNSUPPORTED;
+  if (!ws || ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  EpisodeState* S = static_cast<EpisodeState*>(state);
+  Rec* part = static_cast<Rec*>(ws);
+  const bool rect = integrator == MPC_INTEG_RECT;
+  const bool wide = wide_ok(v_sc, beta_sc, n_cand);
+  const int64_t tiles = cdiv(n_cand, kBlock * (wide ? kCplWide : 1));
+  const int64_t grid = std::min<int64_t>(tiles, kMaxBlocks);
+  const Consts Kdummy{};
+  if (wide) {
+    if (rect) launch_by_steps<kCplWide, MPC_INTEG_RECT, true>(grid, st, Kdummy, v_sc, beta_sc, n_cand, n_steps, tiles, part, &S->K);
+    else launch_by_steps<kCplWide, MPC_INTEG_QK21, true>(grid, st, Kdummy, v_sc, beta_sc, n_cand, n_steps, tiles, part, &S->K);
+  } else {
+    if (rect) launch_by_steps<1, MPC_INTEG_RECT, true>(grid, st, Kdummy, v_sc, beta_sc, n_cand, n_steps, tiles, part, &S->K);
+    else launch_by_steps<1, MPC_INTEG_QK21, true>(grid, st, Kdummy, v_sc, beta_sc, n_cand, n_steps, tiles, part, &S->K);
+  }
+  return last_hip_status();
+}
+
+int mpc_episode_finalize(void* state, const double* v_sc, const double* beta_sc, int64_t n_cand,
+                         int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
+                         size_t ws_bytes, mpc_result_t* out, const mpc_episode_config_t* advance,
+                         mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream) {
+  if (!state || !v_sc || !beta_sc || !out || n_cand < 1 || n_steps < 1 ||
+      n_steps > MPC_MAX_STEPS || index_base < 0)
+    return MPC_ERR_ARG;
+  if (integrator != MPC_INTEG_QK21 && integrator != MPC_INTEG_RECT) return MPC_ERR_UNSUPPORTED;
+  if (!ws || ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  EpisodeState* S = static_cast<EpisodeState*>(state);
+  const Rec* part = static_cast<const Rec*>(ws);
+  const int n_part = static_cast<int>(partial_count(v_sc, beta_sc, n_cand, false));
+  const Consts Kdummy{};
+  if (advance && (check_episode_cfg(advance) != MPC_OK || log_capacity < 0)) return MPC_ERR_ARG;
+  const mpc_episode_config_t ecfg = advance ? *advance : mpc_episode_config_t{};
+  const EpisodeHook hook{advance ? S : nullptr, log, log_capacity};
+  if (integrator == MPC_INTEG_RECT)
+    k_finalize<MPC_INTEG_RECT, true><<<1, kFinBlock, 0, st>>>(
+        part, n_part, Kdummy, &S->K, v_sc, beta_sc, n_cand, n_steps, index_base, 0.0,
+        &S->incumbent, out, ecfg, hook);
+  else
+    k_finalize<MPC_INTEG_QK21, true><<<1, kFinBlock, 0, st>>>(
+        part, n_part, Kdummy, &S->K, v_sc, beta_sc, n_cand, n_steps, index_base, 0.0,
+        &S->incumbent, out, ecfg, hook);
+  return last_hip_status();
+}
+
+int mpc_episode_expand(const mpc_episode_config_t* cfg, void* state, double* v_sc,
+                       double* beta_sc, int64_t n_cand, int32_t n_steps, int64_t index_base,
+                       int32_t integrator, void* ws, size_t ws_bytes, mpc_result_t* out,
+                       mpc_stream_t stream) {
+  int a = check_expand_args(cfg, state, v_sc, beta_sc, n_cand, n_steps, index_base, integrator,
+                            ws, ws_bytes);
+  if (a != MPC_OK) return a;
+  if (!out) return MPC_ERR_ARG;
+  if ((a = mpc_episode_sample(cfg, state, v_sc, beta_sc, n_cand, n_steps, index_base, stream)))
+    return a;
+  if ((a = mpc_episode_partials(state, v_sc, beta_sc, n_cand, n_steps, integrator, ws, ws_bytes,
+                                stream)))
+    return a;
+  return mpc_episode_finalize(state, v_sc, beta_sc, n_cand, n_steps, index_base, integrator, ws,
+                              ws_bytes, out, nullptr, nullptr, 0, stream);
+}
+
+int mpc_episode_advance(const mpc_episode_config_t* cfg, void* state, const mpc_result_t* results,
+                        int32_t n_results, mpc_episode_log_t* log, int32_t log_capacity,
+                        mpc_stream_t stream) {
+  if (check_episode_cfg(cfg) != MPC_OK || !state || !results || n_results < 1 ||
+      log_capacity < 0)
+    return MPC_ERR_ARG;
+  k_episode_advance<<<1, 64, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+      *cfg, static_cast<EpisodeState*>(state), results, n_results, log, log_capacity);
   return last_hip_status();
 }
 

@@ -28,8 +28,15 @@ def shard_range(n_total, rank, world):
 
 
 def gather_results(local_out, group=None):
-    """all_gather of one uint8[RESULT_BYTES] record per rank -> uint8[world*RESULT_BYTES]."""
+    """all_gather of one uint8[RESULT_BYTES] record per rank -> uint8[world*RESULT_BYTES].
+
+    RCCL (backend "nccl") gathers device memory directly.  A gloo group
+    (CPU tests, or rehearsing several ranks on one GPU) stages through host
+    memory."""
     world = dist.get_world_size(group)
+    if local_out.is_cuda and dist.get_backend(group) == "gloo":
+        host = gather_results(local_out.cpu(), group)
+        return host.to(local_out.device)
     gathered = torch.empty(world * RESULT_BYTES, dtype=torch.uint8, device=local_out.device)
     dist.all_gather_into_tensor(gathered, local_out, group=group)
     return gathered

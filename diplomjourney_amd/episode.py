@@ -14,6 +14,7 @@ Per MPC step (one `Episode.step()`):
 The incumbent is sys.maxsize after the first call, as in the reference
 (:428); the episode restarts from the start pose when the target is reached.
 """
+import ctypes
 import math
 import sys
 import time
@@ -21,8 +22,9 @@ import time
 import torch
 
 from . import math_model_tree as mmt
-from .abi import make_problem
-from .distributed import exchange_winner, shard_range
+from .abi import LOG_BYTES, RESULT_BYTES, MpcEpisodeConfig, MpcEpisodeLog, make_problem
+from .distributed import exchange_winner, gather_results, shard_range
+from . import native
 
 
 class Episode:
@@ -76,7 +78,7 @@ class Episode:
             V = [vel] * len(V)
         return V, B
 
-    def step(self, time_kernel=False):
+    def step(self, time_kernel=False, events=None):
         t0 = time.perf_counter()
         V, B = self._grids()
         nv, nb = len(V), len(B)
@@ -90,13 +92,13 @@ class Episode:
                                  beta_out=self.b_sc)
         prob = make_problem(self.x, self.y, self.phi, self.x_t, self.y_t, self.x_0, self.y_0,
                             mmt.L, self.t, self.t + mmt.delta_t)
-        if time_kernel:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record()
+        if time_kernel and events is None:
+            events = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        if events:
+            events[0].record()
         self.eng.partials(prob, self.v_sc, self.b_sc, self.integrator)
-        if time_kernel:
-            e1.record()
+        if events:
+            events[1].record()
         out = self.eng.finalize(prob, self.v_sc, self.b_sc, index_base=self.lo,
                                 incumbent=self.incumbent, integrator=self.integrator,
                                 out=self.eng.result)
@@ -104,7 +106,7 @@ class Episode:
             exchange_winner(self.eng, out, incumbent=self.incumbent, group=self.group)
         res = self.eng.fetch()
         if time_kernel:
-            self.kernel_ms.append(e0.elapsed_time(e1))
+            self.kernel_ms.append(events[0].elapsed_time(events[1]))
         self._advance(res)
         self.step_ms.append((time.perf_counter() - t0) * 1e3)
         return res
@@ -148,6 +150,124 @@ class Episode:
         tx, ty = mmt._turn_target(self.x, self.y, self.phi, 2, sign)
         self._new_target(tx, ty)
         self.steps_for_slowing = 20          # slow_down(radians(90)), :175/:213
+
+
+def reference_episode_config(start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3), seed=20261015,
+                             max_steps=400):
+    """mpc_episode_config_t with the reference's constants and expressions
+    (config.py; grid ratios as math_model_tree.py:241-253 computes them; the
+    operator schedule of :564-569; slow_down bands of :219-226)."""
+    c = mmt._cfg
+    return MpcEpisodeConfig(
+        start_x=start[0], start_y=start[1], start_phi=start[2], start_v=start[3],
+        start_beta=start[4], target_x=target[0], target_y=target[1],
+        L=c.L, delta_t=c.delta_t, eps=c.eps, v_max=c.v_max, v_min=c.v_min, delta_v=c.delta_v,
+        ratio_v=(c.v_acc_max * c.delta_t) / c.delta_v, delta_beta=c.delta_beta,
+        ratio_beta=(math.degrees(c.beta_acc_max) * c.delta_t) / math.degrees(c.delta_beta),
+        beta_bound=c.beta_max + math.radians(c.eps_beta), radius_u_turn=mmt.radius_u_turn,
+        turn_distance=2.0, event_target_x=2.0, event_target_y=3.0,
+        p_turn_right=60, p_turn_left=90, p_new_target=110, slow_new_target=10, slow_turn=20,
+        max_steps=max_steps, seed=seed)
+
+
+class DeviceEpisode:
+    """The same episode with its state in HBM (mpc_episode_* C ABI): a step
+    is enqueued without any host synchronisation, so the host only launches
+    and the GPU runs steps back to back.  `read_log()` syncs and decodes the
+    per-step records."""
+
+    def __init__(self, engine, n_cand_total, n_steps, rank=0, world=1, seed=20261015,
+                 integrator="rect", group=None, start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3),
+                 log_capacity=4096):
+        self.eng = engine
+        self.lib = native.lib()
+        self.n_total = int(n_cand_total)
+        self.n_steps = int(n_steps)
+        self.rank, self.world, self.group = rank, world, group
+        self.lo, self.hi = shard_range(self.n_total, rank, world)
+        self.n_local = self.hi - self.lo
+        self.integrator = integrator
+        self.cfg = reference_episode_config(start, target, seed)
+        dev = engine.device
+        self.state = torch.zeros(self.lib.mpc_episode_state_bytes(), dtype=torch.uint8,
+                                 device=dev)
+        self.v_sc = torch.empty((self.n_steps, self.n_local), dtype=torch.float64, device=dev)
+        self.b_sc = torch.empty_like(self.v_sc)
+        self.local = torch.zeros(RESULT_BYTES, dtype=torch.uint8, device=dev)
+        self.winner = torch.zeros(RESULT_BYTES, dtype=torch.uint8, device=dev)
+        self.log_capacity = int(log_capacity)
+        self.log = torch.zeros(self.log_capacity * LOG_BYTES, dtype=torch.uint8, device=dev)
+        self.ws = torch.empty(self.lib.mpc_workspace_bytes(self.n_local, self.n_steps),
+                              dtype=torch.uint8, device=dev)
+        from .abi import INTEGRATORS
+        self._integ = INTEGRATORS[integrator]
+        self.steps_enqueued = 0
+        self.reset()
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def reset(self):
+        native.check(self.lib.mpc_episode_reset(ctypes.byref(self.cfg), self.state.data_ptr(),
+                                                self._stream()), "mpc_episode_reset")
+        self.steps_enqueued = 0
+
+    def expand(self, events=None):
+        """Grid + sampler + rollout + finalize for this rank's shard.
+        events: optional (start, stop) torch.cuda.Event pair recorded around
+        the streaming rollout kernel alone."""
+        st = self._stream()
+        L = self.lib
+        native.check(L.mpc_episode_sample(ctypes.byref(self.cfg), self.state.data_ptr(),
+                                          self.v_sc.data_ptr(), self.b_sc.data_ptr(),
+                                          self.n_local, self.n_steps, self.lo, st),
+                     "mpc_episode_sample")
+        if events:
+            events[0].record()
+        native.check(L.mpc_episode_partials(self.state.data_ptr(), self.v_sc.data_ptr(),
+                                            self.b_sc.data_ptr(), self.n_local, self.n_steps,
+                                            self._integ, self.ws.data_ptr(), self.ws.numel(), st),
+                     "mpc_episode_partials")
+        if events:
+            events[1].record()
+        fused = self.world == 1    # one GPU: finalize also advances the episode
+        native.check(L.mpc_episode_finalize(self.state.data_ptr(), self.v_sc.data_ptr(),
+                                            self.b_sc.data_ptr(), self.n_local, self.n_steps,
+                                            self.lo, self._integ, self.ws.data_ptr(),
+                                            self.ws.numel(), self.local.data_ptr(),
+                                            ctypes.byref(self.cfg) if fused else None,
+                                            self.log.data_ptr() if fused else None,
+                                            self.log_capacity if fused else 0, st),
+                     "mpc_episode_finalize")
+        if fused:
+            self.steps_enqueued += 1
+
+    def advance(self):
+        """Multi-GPU: all_gather of the per-rank winners (RCCL) + selection +
+        episode update in one launch; no host synchronisation.  (On one GPU
+        the update already ran inside finalize.)"""
+        if self.world == 1:
+            return
+        gathered = gather_results(self.local, self.group)
+        native.check(self.lib.mpc_episode_advance(
+            ctypes.byref(self.cfg), self.state.data_ptr(), gathered.data_ptr(), self.world,
+            self.log.data_ptr(), self.log_capacity, self._stream()), "mpc_episode_advance")
+        self.steps_enqueued += 1
+
+    def step(self, events=None):
+        self.expand(events)
+        self.advance()
+
+    def read_log(self):
+        torch.cuda.current_stream().synchronize()
+        raw = self.log.cpu().numpy().tobytes()
+        n = min(self.steps_enqueued, self.log_capacity)
+        recs = [MpcEpisodeLog.from_buffer_copy(raw[i * LOG_BYTES:(i + 1) * LOG_BYTES])
+                for i in range(self.log_capacity)]
+        # a written record has episode >= 1 (slots never written are zero)
+        recs = [r for r in recs if r.episode >= 1 and r.step < self.steps_enqueued]
+        recs.sort(key=lambda r: r.step)
+        return recs[-n:]
 
 
 def percentile(xs, q):

@@ -12,7 +12,7 @@ import os
 import subprocess
 import sys
 
-from .abi import MpcError, MpcProblem
+from .abi import MpcEpisodeConfig, MpcError, MpcProblem
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
@@ -28,7 +28,9 @@ EXPORTS = (
     "mpc_version", "mpc_strerror", "mpc_workspace_bytes", "mpc_rollout_argmin",
     "mpc_rollout_partials", "mpc_rollout_finalize",
     "mpc_batched_workspace_bytes", "mpc_rollout_argmin_batched", "mpc_select_winner",
-    "mpc_sample_controls",
+    "mpc_sample_controls", "mpc_episode_state_bytes", "mpc_episode_reset",
+    "mpc_episode_expand", "mpc_episode_advance", "mpc_episode_sample", "mpc_episode_partials",
+    "mpc_episode_finalize",
 )
 
 HIPCC_FLAGS = [
@@ -101,6 +103,24 @@ def lib():
     L.mpc_sample_controls.restype = ctypes.c_int
     L.mpc_sample_controls.argtypes = [_P, _I32, _P, _I32, _I64, _I32, ctypes.c_uint64, _I64,
                                       _I32, _P, _P, _I64, _P]
+    L.mpc_episode_state_bytes.restype = ctypes.c_size_t
+    L.mpc_episode_state_bytes.argtypes = []
+    L.mpc_episode_reset.restype = ctypes.c_int
+    L.mpc_episode_reset.argtypes = [ctypes.POINTER(MpcEpisodeConfig), _P, _P]
+    L.mpc_episode_expand.restype = ctypes.c_int
+    L.mpc_episode_expand.argtypes = [ctypes.POINTER(MpcEpisodeConfig), _P, _P, _P, _I64, _I32,
+                                     _I64, _I32, _P, ctypes.c_size_t, _P, _P]
+    L.mpc_episode_advance.restype = ctypes.c_int
+    L.mpc_episode_advance.argtypes = [ctypes.POINTER(MpcEpisodeConfig), _P, _P, _I32, _P, _I32,
+                                      _P]
+    L.mpc_episode_sample.restype = ctypes.c_int
+    L.mpc_episode_sample.argtypes = [ctypes.POINTER(MpcEpisodeConfig), _P, _P, _P, _I64, _I32,
+                                     _I64, _P]
+    L.mpc_episode_partials.restype = ctypes.c_int
+    L.mpc_episode_partials.argtypes = [_P, _P, _P, _I64, _I32, _I32, _P, ctypes.c_size_t, _P]
+    L.mpc_episode_finalize.restype = ctypes.c_int
+    L.mpc_episode_finalize.argtypes = [_P, _P, _P, _I64, _I32, _I64, _I32, _P, ctypes.c_size_t,
+                                       _P, ctypes.POINTER(MpcEpisodeConfig), _P, _I32, _P]
     _lib = L
     return L
 

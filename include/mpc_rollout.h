@@ -133,6 +133,66 @@ int mpc_sample_controls(const double* v_grid, int32_t n_v, const double* beta_gr
                         int64_t index_base, int32_t const_prefix, double* v_sc,
                         double* beta_sc, int64_t ld, mpc_stream_t stream);
 
+
+/* ---------------------------------------------------------------------------
+ * Device-resident MPC episode: the reference's math_mpc loop
+ * (math_model_tree.py:515-635) with its state in HBM, so an MPC step is
+ * enqueued with no host synchronisation (graph-capturable):
+ *   mpc_episode_expand   grid (:239-256, slow-down :312-316) + t += dt
+ *                        (:302) + sampler + rollout + finalize -> local winner
+ *   mpc_episode_advance  [multi-GPU: over the all_gather'ed per-rank winners,
+ *                        lexicographic (cost, index) selection first]
+ *                        finishing logic (:392-414), operator events
+ *                        (:564-569), arrival/step-limit restart, one log record
+ * On one GPU, mpc_episode_finalize can apply the advance itself (`advance`
+ * non-NULL), so a step is three launches.
+ * The grid ratios are passed precomputed with the reference's expressions.
+ * ------------------------------------------------------------------------- */
+typedef struct mpc_episode_config {
+  double start_x, start_y, start_phi, start_v, start_beta; /* initial_coordinates (:736)   */
+  double target_x, target_y;                               /* target_coordinates           */
+  double L, delta_t, eps;                                  /* config.py                    */
+  double v_max, v_min, delta_v, ratio_v;      /* ratio_v = (v_acc_max*delta_t)/delta_v      */
+  double delta_beta, ratio_beta, beta_bound;  /* ratio_beta = degrees(beta_acc_max)*delta_t /
+                                                 degrees(delta_beta); beta_bound = beta_max +
+                                                 radians(eps_beta)                 (:249-256) */
+  double radius_u_turn, turn_distance;                     /* :44; distance 2 (:565-567)   */
+  double event_target_x, event_target_y;                   /* new_target(..., 2, 3) (:569) */
+  int32_t p_turn_right, p_turn_left, p_new_target;         /* 60, 90, 110; <= 0 disables   */
+  int32_t slow_new_target, slow_turn;                      /* slow_down(): 10, 20          */
+  int32_t max_steps;                                       /* restart after this many      */
+  uint64_t seed;                                           /* candidate sampler seed       */
+} mpc_episode_config_t;
+
+typedef struct mpc_episode_log {
+  int64_t step;          /* global MPC step counter                     */
+  int64_t index;         /* chosen candidate (global), -1 if none       */
+  int32_t p, episode;    /* iteration number within the episode         */
+  double cost, x, y, phi, v, beta;   /* chosen cost and the state moved to */
+} mpc_episode_log_t;
+
+size_t mpc_episode_state_bytes(void);
+int mpc_episode_reset(const mpc_episode_config_t* cfg, void* state, mpc_stream_t stream);
+int mpc_episode_expand(const mpc_episode_config_t* cfg, void* state, double* v_sc,
+                       double* beta_sc, int64_t n_cand, int32_t n_steps, int64_t index_base,
+                       int32_t integrator, void* ws, size_t ws_bytes, mpc_result_t* out,
+                       mpc_stream_t stream);
+int mpc_episode_advance(const mpc_episode_config_t* cfg, void* state, const mpc_result_t* results,
+                        int32_t n_results, mpc_episode_log_t* log, int32_t log_capacity,
+                        mpc_stream_t stream);
+/* The three launches of mpc_episode_expand, separately (timing, overlap):
+ * grid + t + problem + sampler | streaming rollout kernel | selection. */
+int mpc_episode_sample(const mpc_episode_config_t* cfg, void* state, double* v_sc,
+                       double* beta_sc, int64_t n_cand, int32_t n_steps, int64_t index_base,
+                       mpc_stream_t stream);
+int mpc_episode_partials(void* state, const double* v_sc, const double* beta_sc, int64_t n_cand,
+                         int32_t n_steps, int32_t integrator, void* ws, size_t ws_bytes,
+                         mpc_stream_t stream);
+int mpc_episode_finalize(void* state, const double* v_sc, const double* beta_sc, int64_t n_cand,
+                         int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
+                         size_t ws_bytes, mpc_result_t* out, const mpc_episode_config_t* advance,
+                         mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -278,3 +278,29 @@ def test_two_phase_api_matches(engine):
     engine.finalize(prob, v, b, integrator="rect")
     two = engine.fetch()
     assert bytes(one) == bytes(two)
+
+
+def test_device_episode_matches_host_episode(engine):
+    """The device-resident episode (mpc_episode_*: grid, sampler, problem,
+    finishing logic and operator events in HBM, no host sync) makes the same
+    choices as the host-driven episode over 200 MPC steps incl. the
+    p = 60 / 90 / 110 operator events."""
+    from diplomjourney_amd.episode import DeviceEpisode, Episode
+    n, ns, steps = 20_000, 10, 200
+    host = Episode(engine, n, ns)
+    want = []
+    for _ in range(steps):
+        p = host.p
+        r = host.step()
+        want.append((r.index if r.found else -1, r.cost, p, host.x, host.y, host.phi, host.v,
+                     host.beta))
+    dev = DeviceEpisode(engine, n, ns, log_capacity=512)
+    for _ in range(steps):
+        dev.step()
+    got = dev.read_log()
+    assert len(got) == steps
+    for g, w in zip(got, want):
+        assert (g.index, g.p) == (w[0], w[2])
+        assert math.isclose(g.cost, w[1], rel_tol=COST_RTOL)
+        assert max(abs(a - b) for a, b in zip((g.x, g.y, g.phi, g.v, g.beta), w[3:])) <= STATE_TOL
+    assert max(w[2] for w in want) > 110          # the operator events were exercised
