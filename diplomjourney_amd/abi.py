@@ -17,7 +17,13 @@ MPC_ERR_UNSUPPORTED = -4
 MPC_INTEG_QK21 = 0
 MPC_INTEG_RECT = 1
 
-INTEGRATORS = {"qk21": MPC_INTEG_QK21, "rect": MPC_INTEG_RECT}
+MPC_HEADING_ROTATE = 0x100
+
+# integrator argument of the C ABI: QUADPACK-exact or exact integral, each
+# with the heading evaluated directly (reference formula) or by rotation
+INTEGRATORS = {"qk21": MPC_INTEG_QK21, "rect": MPC_INTEG_RECT,
+               "qk21+rot": MPC_INTEG_QK21 | MPC_HEADING_ROTATE,
+               "rect+rot": MPC_INTEG_RECT | MPC_HEADING_ROTATE}
 
 
 class MpcProblem(ctypes.Structure):

@@ -26,6 +26,7 @@ struct Consts {
   double L, inv_L;         // wheelbase; 1/L when L is a power of two
   double h;                // (t+dt) - t, the quad interval length (RECT)
   double hlgth;            // 0.5*((t+dt) - t), QUADPACK's half length (QK21)
+  double s0, c0;            // sin/cos of phi (heading-rotation mode)
   int32_t L_pow2;          // v/L == v*inv_L exactly
   int32_t pad_;
 };
@@ -57,16 +58,47 @@ MPC_HD __forceinline__ double quad_const(double f, const Consts& K) {
 
 // iteration_of_predict (math_model_tree.py:111-115): heading first, then
 // position with the updated heading (semi-implicit bicycle step).
-template <int INTEG>
-MPC_HD __forceinline__ void step(double& x, double& y, double& ph, double v, double beta,
-                                 const Consts& K) {
+//
+// step_core is the hot-loop form.  It uses the range-limited trig cores and
+// flags the candidate `bad` when an argument leaves their range (|beta| or,
+// in direct mode, |phi| > kFastMax; in rotation mode |dphi| > kRotMax; NaN).
+// A bad candidate is recomputed with step_safe (direct sin/cos, library
+// fallbacks), so every candidate gets a well-defined, correct result while the
+// hot loop carries no fallback code.
+//   ROT = false: sin/cos of the new heading evaluated directly (the reference's
+//                formula, :113-114)
+//   ROT = true:  (s, c) carry sin/cos of the heading and are rotated by the
+//                increment (mpc_trig.h rotation_factors / rotate_by)
+template <int INTEG, bool ROT>
+MPC_HD __forceinline__ void step_core(double& x, double& y, double& ph, double& s, double& c,
+                                      double v, double beta, const Consts& K, bool& bad) {
+  bad |= !(fabs(beta) <= trig::kFastMax);
   const double w = K.L_pow2 ? v * K.inv_L : v / K.L;          // _velocity / L   (:78)
-  const double dphi = quad_const<INTEG>(w * trig::tan_fast(beta), K);  // angle_phi (:107)
+  const double dphi = quad_const<INTEG>(w * trig::tan_core(beta), K);  // angle_phi (:107)
   ph = ph + dphi;                                              // phi + _phi      (:113)
-  double s, c;
-  trig::sincos_fast(ph, &s, &c);
+  if constexpr (ROT) {
+    bad |= !(fabs(dphi) <= trig::kRotMax);
+    double sd, cm1;
+    trig::rotation_factors(dphi, sd, cm1);
+    trig::rotate_by(sd, cm1, s, c);
+  } else {
+    bad |= !(fabs(ph) <= trig::kFastMax);
+    trig::sincos_core(ph, &s, &c);
+  }
   x = x + quad_const<INTEG>(v * c, K);                         // coordinate_x    (:99)
   y = y + quad_const<INTEG>(v * s, K);                         // coordinate_y    (:103)
+}
+
+template <int INTEG>
+MPC_HD __forceinline__ void step_safe(double& x, double& y, double& ph, double v, double beta,
+                                      const Consts& K) {
+  const double w = K.L_pow2 ? v * K.inv_L : v / K.L;
+  const double dphi = quad_const<INTEG>(w * trig::tan_fast(beta), K);
+  ph = ph + dphi;
+  double s, c;
+  trig::sincos_fast(ph, &s, &c);
+  x = x + quad_const<INTEG>(v * c, K);
+  y = y + quad_const<INTEG>(v * s, K);
 }
 
 // control_criterion (math_model_tree.py:82-87) on the layer-N state.
@@ -80,6 +112,39 @@ MPC_HD __forceinline__ double cost(double x, double y, const Consts& K) {
     d = fabs(K.A * x - K.B * y + K.C1 - K.C2) / K.den;         // :60-61
   }
   return 10000.0 * dist_target + 10000.0 * (d * d);            // :62, :87
+}
+
+// One candidate, exactly as the kernels evaluate it (the host replica in
+// tests/replica_harness.cpp calls this): the core recurrence, and if that
+// flags the candidate, the safe recurrence.  traj (optional) gets the
+// per-step (x, y, phi).  Returns the cost.
+template <int INTEG, bool ROT>
+MPC_HD inline double rollout_candidate(const Consts& K, const double* v, const double* b,
+                                       int64_t ld, int64_t col, int n_steps, double* traj) {
+  double x = K.x, y = K.y, ph = K.phi, s = K.s0, c = K.c0;
+  bool bad = false;
+  for (int st = 0; st < n_steps; ++st) {
+    step_core<INTEG, ROT>(x, y, ph, s, c, v[st * ld + col], b[st * ld + col], K, bad);
+    if (traj) {
+      traj[3 * st + 0] = x;
+      traj[3 * st + 1] = y;
+      traj[3 * st + 2] = ph;
+    }
+  }
+  if (bad) {
+    x = K.x;
+    y = K.y;
+    ph = K.phi;
+    for (int st = 0; st < n_steps; ++st) {
+      step_safe<INTEG>(x, y, ph, v[st * ld + col], b[st * ld + col], K);
+      if (traj) {
+        traj[3 * st + 0] = x;
+        traj[3 * st + 1] = y;
+        traj[3 * st + 2] = ph;
+      }
+    }
+  }
+  return cost(x, y, K);
 }
 
 // Total order on costs for the arg-min: non-finite costs (NaN, +inf) map to

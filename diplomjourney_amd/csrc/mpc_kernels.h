@@ -1,0 +1,490 @@
+// mpc_kernels.h — the rollout / arg-min / selection / sampling kernels (gfx950).
+//
+//   k_rollout_argmin   one lane per CPL adjacent candidates (CPL = 2: every
+//                      control load is 16 B per lane = 1 KiB per wave
+//                      instruction); N-step rollout in registers with the next
+//                      step's controls in flight; terminal cost; lane -> wave
+//                      (shuffle) -> block (LDS) lexicographic (cost, index)
+//                      arg-min; one 16-B record per block.
+//   k_finalize         arg-min over the block records; the winner re-rolled
+//                      lane-parallel (bitwise the arithmetic the lane scored).
+//   k_rollout_argmin_batched / k_finalize_batched   robot-segmented variant.
+//   k_select_winner    lexicographic min over gathered per-rank results.
+//   k_sample_controls  synthetic control sequences (splitmix64 -> grid entry).
+//
+// Template modes: INTEG (MPC_INTEG_QK21 | MPC_INTEG_RECT), ROT (heading
+// rotation recurrence instead of a per-step sincos), STATES (write every
+// candidate's per-step states: the CoordinateTree payload), KDEV (problem
+// constants read from device memory: the device-resident episode).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mpc_rollout.h"
+#include "mpc_device.h"
+
+namespace mpc {
+
+constexpr int kBlock = 256;  // 4 waves of 64
+// Build-time tuning knobs (A/B-tested with tools/probe_gpu.py variants):
+#ifndef MPC_CPL
+#define MPC_CPL 2            // candidates per lane on the aligned path (2 or 4)
+#endif
+#ifndef MPC_MIN_WAVES
+#define MPC_MIN_WAVES 1      // __launch_bounds__ minimum waves per SIMD
+#endif
+constexpr int kCplWide = MPC_CPL;
+static_assert(kCplWide == 2 || kCplWide == 4, "MPC_CPL must be 2 or 4");
+constexpr int kWaves = kBlock / 64;
+constexpr int64_t kMaxBlocks = 2048;  // 256 CUs x 8 resident blocks upper bound
+constexpr int kFinBlock = 1024;
+
+struct Rec {
+  uint64_t key;
+  int64_t idx;
+};
+
+// Block-level arg-min: wave shuffle, then the kWaves wave records via LDS.
+// The block winner ends up in thread 0.
+__device__ __forceinline__ void block_argmin(uint64_t& k, int64_t& i) {
+  __shared__ uint64_t s_key[kWaves];
+  __shared__ int64_t s_idx[kWaves];
+  wave_argmin(k, i);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    s_key[wave] = k;
+    s_idx[wave] = i;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w)
+      if (rec_less(s_key[w], s_idx[w], k, i)) {
+        k = s_key[w];
+        i = s_idx[w];
+      }
+  }
+}
+
+// Rollout of CPL adjacent candidates starting at column c0; costs in cst.
+template <int CPL, int INTEG, bool ROT, bool STATES>
+__device__ __forceinline__ void rollout_lane(const Consts& K, const double* __restrict__ v,
+                                             const double* __restrict__ b, int64_t ld, int64_t c0,
+                                             int n_steps, double (&cst)[CPL],
+                                             double* __restrict__ states, int64_t n_cand) {
+  double x[CPL], y[CPL], ph[CPL], sn[CPL], cs[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    x[j] = K.x;
+    y[j] = K.y;
+    ph[j] = K.phi;
+    sn[j] = K.s0;
+    cs[j] = K.c0;
+  }
+  // Controls of step sr for this lane's CPL candidates: 16 B per lane per
+  // array on the wide path (one 1 KiB wave-instruction each).
+  auto load = [&](int sr, double (&vv)[CPL], double (&bb)[CPL]) {
+    if constexpr (CPL >= 2) {
+#pragma unroll
+      for (int h = 0; h < CPL; h += 2) {
+        const double2 v2 = *reinterpret_cast<const double2*>(v + sr * ld + c0 + h);
+        const double2 b2 = *reinterpret_cast<const double2*>(b + sr * ld + c0 + h);
+        vv[h] = v2.x;
+        vv[h + 1] = v2.y;
+        bb[h] = b2.x;
+        bb[h + 1] = b2.y;
+      }
+    } else {
+      vv[0] = v[sr * ld + c0];
+      bb[0] = b[sr * ld + c0];
+    }
+  };
+  bool bad[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) bad[j] = false;
+  auto body = [&](int sr, const double (&vv)[CPL], const double (&bb)[CPL]) {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      step_core<INTEG, ROT>(x[j], y[j], ph[j], sn[j], cs[j], vv[j], bb[j], K, bad[j]);
+      if constexpr (STATES) {
+        states[(sr * 3 + 0) * n_cand + c0 + j] = x[j];
+        states[(sr * 3 + 1) * n_cand + c0 + j] = y[j];
+        states[(sr * 3 + 2) * n_cand + c0 + j] = ph[j];
+      }
+    }
+  };
+  // Software pipeline, two steps per trip (ping-pong registers, no copies):
+  // the next step's controls are in flight while this step's trig chain runs
+  // (the HBM latency is about one step of VALU work).
+  double va[CPL], ba[CPL], vb[CPL], bb_[CPL];
+  load(0, va, ba);
+#pragma unroll 1
+  for (int s = 0; s < n_steps; s += 2) {
+    if (s + 1 < n_steps) load(s + 1, vb, bb_);
+    body(s, va, ba);
+    if (s + 1 < n_steps) {
+      if (s + 2 < n_steps) load(s + 2, va, ba);
+      body(s + 1, vb, bb_);
+    }
+  }
+  // Irregular candidates (argument outside the trig cores' range, or NaN):
+  // recompute with the safe recurrence.  Never taken for the reference's
+  // arguments; kept out of the loop so the loop carries no fallback code.
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    if (bad[j]) {
+      x[j] = K.x;
+      y[j] = K.y;
+      ph[j] = K.phi;
+      for (int sr = 0; sr < n_steps; ++sr) {
+        step_safe<INTEG>(x[j], y[j], ph[j], v[sr * ld + c0 + j], b[sr * ld + c0 + j], K);
+        if constexpr (STATES) {
+          states[(sr * 3 + 0) * n_cand + c0 + j] = x[j];
+          states[(sr * 3 + 1) * n_cand + c0 + j] = y[j];
+          states[(sr * 3 + 2) * n_cand + c0 + j] = ph[j];
+        }
+      }
+    }
+    cst[j] = cost(x[j], y[j], K);
+  }
+}
+
+template <int CPL, int INTEG, bool ROT, bool STATES, bool KDEV>
+__global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(
+    Consts Karg, const Consts* __restrict__ Kdev, const double* __restrict__ v,
+    const double* __restrict__ b, int64_t n_cand, int n_steps, int64_t n_tiles,
+    Rec* __restrict__ part, double* __restrict__ states) {
+  const Consts K = KDEV ? *Kdev : Karg;
+  uint64_t best_k = ~0ull;
+  int64_t best_i = INT64_MAX;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int64_t c0 = tile * (kBlock * CPL) + threadIdx.x * CPL;
+    if (c0 < n_cand) {  // CPL > 1 requires n_cand % CPL == 0: the whole group is valid
+      double cst[CPL];
+      rollout_lane<CPL, INTEG, ROT, STATES>(K, v, b, n_cand, c0, n_steps, cst, states, n_cand);
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        const uint64_t kk = cost_key(cst[j]);
+        if (kk < best_k) {  // ascending index per lane: strict < keeps the first
+          best_k = kk;
+          best_i = c0 + j;
+        }
+      }
+    }
+  }
+  block_argmin(best_k, best_i);
+  if (threadIdx.x == 0) part[blockIdx.x] = Rec{best_k, best_i};
+}
+
+// Re-roll the winner and fill the result record.  Called by ALL threads of
+// the block once thread 0 holds the winner (key, col).  The N-step recurrence
+// is split so that only cheap accumulations stay serial: lane s computes the
+// state-free heading increment dphi_s = Q((v_s/L) tan(beta_s)); lane 0
+// accumulates the headings; lane s evaluates sincos(phi_s) (direct mode) or
+// the rotation factors of dphi_s (ROT); lane 0 rotates (ROT) and accumulates
+// x and y.  The winner is regular or irregular exactly as in rollout_lane
+// (same tests), and each branch repeats that path's operations in the same
+// order, so the emitted states are bitwise those the arg-min scored.
+template <int INTEG, bool ROT>
+__device__ void emit_winner(const Consts& K, const double* __restrict__ v,
+                            const double* __restrict__ b, int64_t ld, int n_steps, uint64_t key,
+                            int64_t col, int64_t reported_index, double incumbent,
+                            mpc_result_t* __restrict__ out) {
+  __shared__ double s_v[MPC_MAX_STEPS], s_dphi[MPC_MAX_STEPS], s_phi[MPC_MAX_STEPS];
+  __shared__ double s_a[MPC_MAX_STEPS], s_c[MPC_MAX_STEPS];
+  __shared__ double s_b0;
+  __shared__ uint64_t s_key;
+  __shared__ int64_t s_col, s_rep;
+  __shared__ int s_bad;
+  if (threadIdx.x == 0) {
+    s_key = key;
+    s_col = col;
+    s_rep = reported_index;
+    s_bad = 0;
+  }
+  __syncthreads();
+  key = s_key;
+  col = s_col;
+  const int lane = threadIdx.x;
+  const bool valid = key != ~0ull;
+  if (valid && lane < n_steps) {
+    const double vs = v[lane * ld + col];
+    const double bs = b[lane * ld + col];
+    s_v[lane] = vs;
+    if (lane == 0) s_b0 = bs;
+    const double w = K.L_pow2 ? vs * K.inv_L : vs / K.L;
+    const double d = quad_const<INTEG>(w * trig::tan_fast(bs), K);  // == tan_core if regular
+    s_dphi[lane] = d;
+    if (!(fabs(bs) <= trig::kFastMax) || (ROT && !(fabs(d) <= trig::kRotMax))) s_bad = 1;
+  }
+  __syncthreads();
+  if (valid && lane == 0) {
+    double ph = K.phi;
+    for (int st = 0; st < n_steps; ++st) {
+      ph = ph + s_dphi[st];
+      s_phi[st] = ph;
+      if (!ROT && !(fabs(ph) <= trig::kFastMax)) s_bad = 1;
+    }
+  }
+  __syncthreads();
+  const bool bad = s_bad != 0;
+  if (valid && lane < n_steps) {
+    if (ROT && !bad)
+      trig::rotation_factors(s_dphi[lane], s_a[lane], s_c[lane]);
+    else
+      trig::sincos_fast(s_phi[lane], &s_a[lane], &s_c[lane]);  // == sincos_core if regular
+  }
+  __syncthreads();
+  if (lane != 0) return;
+  out->n_steps = n_steps;
+  if (!valid) {
+    out->cost = __builtin_inf();
+    out->index = -1;
+    out->found = 0;
+    out->v = 0.0;
+    out->beta = 0.0;
+    return;
+  }
+  const double c = key_cost(key);
+  out->cost = c;
+  out->index = s_rep;
+  out->found = c < incumbent ? 1 : 0;
+  out->v = s_v[0];
+  out->beta = s_b0;
+  double x = K.x, y = K.y, sn = K.s0, cs = K.c0;
+  for (int st = 0; st < n_steps; ++st) {
+    if (ROT && !bad) {
+      trig::rotate_by(s_a[st], s_c[st], sn, cs);
+    } else {
+      sn = s_a[st];
+      cs = s_c[st];
+    }
+    x = x + quad_const<INTEG>(s_v[st] * cs, K);
+    y = y + quad_const<INTEG>(s_v[st] * sn, K);
+    out->traj[st][0] = x;
+    out->traj[st][1] = y;
+    out->traj[st][2] = s_phi[st];
+  }
+}
+
+struct EpisodeState;
+struct EpisodeHook {  // single-GPU episode: finalize also advances it
+  EpisodeState* S;    // nullptr: no hook
+  mpc_episode_log_t* log;
+  int cap;
+};
+__device__ void episode_hook(const mpc_episode_config_t& c, const EpisodeHook& h,
+                             const mpc_result_t& r);
+
+template <int INTEG, bool ROT, bool KDEV>
+__global__ __launch_bounds__(kFinBlock) void k_finalize(
+    const Rec* __restrict__ part, int n_part, Consts Karg, const Consts* __restrict__ Kdev,
+    const double* __restrict__ v, const double* __restrict__ b, int64_t n_cand, int n_steps,
+    int64_t index_base, double incumbent_arg, const double* __restrict__ incumbent_dev,
+    mpc_result_t* __restrict__ out, mpc_episode_config_t ecfg, EpisodeHook hook) {
+  const Consts K = KDEV ? *Kdev : Karg;
+  const double incumbent = KDEV ? *incumbent_dev : incumbent_arg;
+  __shared__ uint64_t s_key[kFinBlock / 64];
+  __shared__ int64_t s_idx[kFinBlock / 64];
+  uint64_t k = ~0ull;
+  int64_t i = INT64_MAX;
+  for (int p = threadIdx.x; p < n_part; p += kFinBlock)
+    if (rec_less(part[p].key, part[p].idx, k, i)) {
+      k = part[p].key;
+      i = part[p].idx;
+    }
+  wave_argmin(k, i);
+  if ((threadIdx.x & 63) == 0) {
+    s_key[threadIdx.x >> 6] = k;
+    s_idx[threadIdx.x >> 6] = i;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kFinBlock / 64; ++w)
+      if (rec_less(s_key[w], s_idx[w], k, i)) {
+        k = s_key[w];
+        i = s_idx[w];
+      }
+  }
+  emit_winner<INTEG, ROT>(K, v, b, n_cand, n_steps, k, i, index_base + i, incumbent, out);
+  if (KDEV && hook.S && threadIdx.x == 0) episode_hook(ecfg, hook, *out);
+}
+
+// Problem constants derived on the device (batched robots, episode).  The
+// squares are x*x (glibc pow(x, 2.0) differs by 1 ulp in ~0.1% of inputs);
+// the single-problem host path derives them with libm pow.
+__device__ __forceinline__ Consts consts_from_problem(const mpc_problem_t& p) {
+  Consts K;
+  K.x = p.x;
+  K.y = p.y;
+  K.phi = p.phi;
+  K.x_t = p.x_t;
+  K.y_t = p.y_t;
+  K.x_0 = p.x_0;
+  K.y_0 = p.y_0;
+  K.A = p.y_t - p.y_0;
+  K.B = p.x_t - p.x_0;
+  K.C1 = p.x_t * p.y_0;
+  K.C2 = p.y_t * p.x_0;
+  K.den = sqrt(K.A * K.A + K.B * K.B);
+  K.L = p.L;
+  int e;
+  const double m = frexp(p.L, &e);
+  K.L_pow2 = (m == 0.5) ? 1 : 0;
+  K.inv_L = K.L_pow2 ? 1.0 / p.L : 0.0;
+  K.h = p.t_b - p.t_a;
+  K.hlgth = 0.5 * (p.t_b - p.t_a);
+  trig::sincos_fast(p.phi, &K.s0, &K.c0);
+  K.pad_ = 0;
+  return K;
+}
+
+// --------------------------- batched robots --------------------------------
+template <int CPL, int INTEG, bool ROT>
+__global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin_batched(
+    const mpc_problem_t* __restrict__ probs, const double* __restrict__ v,
+    const double* __restrict__ b, int64_t cand, int n_steps, int64_t ld, Rec* __restrict__ part) {
+  const int r = blockIdx.y;
+  const Consts K = consts_from_problem(probs[r]);
+  uint64_t best_k = ~0ull;
+  int64_t best_i = INT64_MAX;
+  const int64_t tiles = (cand + kBlock * CPL - 1) / (kBlock * CPL);
+  for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const int64_t cl = tile * (kBlock * CPL) + threadIdx.x * CPL;  // local index
+    if (cl < cand) {
+      double cst[CPL];
+      rollout_lane<CPL, INTEG, ROT, false>(K, v, b, ld, r * cand + cl, n_steps, cst, nullptr, 0);
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        const uint64_t kk = cost_key(cst[j]);
+        if (kk < best_k) {
+          best_k = kk;
+          best_i = cl + j;
+        }
+      }
+    }
+  }
+  block_argmin(best_k, best_i);
+  if (threadIdx.x == 0)
+    part[static_cast<int64_t>(r) * gridDim.x + blockIdx.x] = Rec{best_k, best_i};
+}
+
+template <int INTEG, bool ROT>
+__global__ __launch_bounds__(kBlock) void k_finalize_batched(
+    const Rec* __restrict__ part, int n_part, const mpc_problem_t* __restrict__ probs,
+    const double* __restrict__ incumbents, const double* __restrict__ v,
+    const double* __restrict__ b, int64_t cand, int n_steps, int64_t ld,
+    mpc_result_t* __restrict__ out) {
+  const int r = blockIdx.x;
+  uint64_t k = ~0ull;
+  int64_t i = INT64_MAX;
+  for (int p = threadIdx.x; p < n_part; p += kBlock) {
+    const Rec q = part[static_cast<int64_t>(r) * n_part + p];
+    if (rec_less(q.key, q.idx, k, i)) {
+      k = q.key;
+      i = q.idx;
+    }
+  }
+  block_argmin(k, i);
+  const Consts K = consts_from_problem(probs[r]);
+  const double inc = incumbents ? incumbents[r] : __builtin_inf();
+  emit_winner<INTEG, ROT>(K, v, b, ld, n_steps, k, r * cand + i, i, inc, &out[r]);
+}
+
+// --------------------------- exchange ----------------------------------------
+// Lexicographic (cost, global index) min over n gathered per-rank results.
+__device__ int select_index(const mpc_result_t* __restrict__ res, int n, uint64_t& bk) {
+  int best = 0;
+  int64_t bi = INT64_MAX;
+  bk = ~0ull;
+  for (int r = 0; r < n; ++r) {
+    const uint64_t k = res[r].index < 0 ? ~0ull : cost_key(res[r].cost);
+    const int64_t i = res[r].index < 0 ? INT64_MAX : res[r].index;
+    if (r == 0 || rec_less(k, i, bk, bi)) {
+      best = r;
+      bk = k;
+      bi = i;
+    }
+  }
+  return best;
+}
+
+__global__ void k_select_winner(const mpc_result_t* __restrict__ res, int n, double incumbent,
+                                mpc_result_t* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t bk;
+  const int best = select_index(res, n, bk);
+  *out = res[best];
+  out->found = (bk != ~0ull && out->cost < incumbent) ? 1 : 0;
+}
+
+// --------------------------- sampler -----------------------------------------
+// Grid entry of one (step, candidate): candidate g < n_grid of the constant
+// prefix is the reference's enumeration k = g; otherwise the top 32 bits of
+// splitmix64(seed ^ s<<40 ^ g) are mapped onto [0, n_grid) by multiply-shift
+// (Lemire's fastrange: no integer division on the VALU).
+__device__ __forceinline__ uint32_t grid_entry(uint64_t seed, int s, uint64_t g, uint32_t n_grid,
+                                               int cprefix) {
+  if (cprefix && g < n_grid) return static_cast<uint32_t>(g);
+  const uint64_t h = splitmix64(seed ^ (static_cast<uint64_t>(s) << 40) ^ g);
+  return static_cast<uint32_t>(((h >> 32) * static_cast<uint64_t>(n_grid)) >> 32);
+}
+
+constexpr int kSampleLdsEntries = 2048;  // expanded (v, beta) grid staged in LDS
+
+// One thread per candidate pair (16-B stores), looping over the steps.  The
+// grid |V| x |B| (<= 451 entries for the reference's acceleration limits) is
+// expanded once per block into LDS, so the per-element lookup is one
+// ds_read_b128 instead of a division by |B| and two loads.
+__device__ void sample_items(const double2* s_grid, uint32_t n_grid, int64_t n_cand, int n_steps,
+                             uint64_t seed, int64_t base, int cprefix, double* __restrict__ v,
+                             double* __restrict__ b, int64_t ld, int pairs) {
+  const int cpt = pairs ? 2 : 1;
+  const int64_t n_items = n_cand / cpt;
+  for (int64_t it = blockIdx.x * static_cast<int64_t>(kBlock) + threadIdx.x; it < n_items;
+       it += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const int64_t c = it * cpt;
+    const uint64_t g = static_cast<uint64_t>(base + c);
+    for (int st = 0; st < n_steps; ++st) {
+      const double2 e0 = s_grid[grid_entry(seed, st, g, n_grid, cprefix)];
+      if (pairs) {
+        const double2 e1 = s_grid[grid_entry(seed, st, g + 1, n_grid, cprefix)];
+        *reinterpret_cast<double2*>(v + st * ld + c) = make_double2(e0.x, e1.x);
+        *reinterpret_cast<double2*>(b + st * ld + c) = make_double2(e0.y, e1.y);
+      } else {
+        v[st * ld + c] = e0.x;
+        b[st * ld + c] = e0.y;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_sample_controls(
+    const double* __restrict__ vg, int nv, const double* __restrict__ bg, int nb, int64_t n_cand,
+    int n_steps, uint64_t seed, int64_t base, int cprefix, double* __restrict__ v,
+    double* __restrict__ b, int64_t ld, int pairs) {
+  __shared__ double2 s_grid[kSampleLdsEntries];
+  const uint32_t n_grid = static_cast<uint32_t>(nv) * static_cast<uint32_t>(nb);
+  if (n_grid > kSampleLdsEntries) {
+    // large grids: direct lookups (one division per element)
+    const int cpt = pairs ? 2 : 1;
+    for (int64_t it = blockIdx.x * static_cast<int64_t>(kBlock) + threadIdx.x; it < n_cand / cpt;
+         it += static_cast<int64_t>(gridDim.x) * kBlock) {
+      const int64_t c = it * cpt;
+      for (int st = 0; st < n_steps; ++st)
+        for (int j = 0; j < cpt; ++j) {
+          const uint32_t k = grid_entry(seed, st, base + c + j, n_grid, cprefix);
+          v[st * ld + c + j] = vg[k / nb];
+          b[st * ld + c + j] = bg[k % nb];
+        }
+    }
+    return;
+  }
+  for (uint32_t k = threadIdx.x; k < n_grid; k += kBlock)
+    s_grid[k] = make_double2(vg[k / nb], bg[k % nb]);
+  __syncthreads();
+  sample_items(s_grid, n_grid, n_cand, n_steps, seed, base, cprefix, v, b, ld, pairs);
+}
+
+}  // namespace mpc

@@ -57,10 +57,13 @@ constexpr double kT[16] = {0x1.090dd50c4e26cp-18, -0x1.46ffa51d98a1ep-17, 0x1.47
 // (loop-invariant) coefficient into the accumulator first: two VALU ops and
 // two VGPRs per coefficient.  The three-address VOP3 form with the
 // coefficient in an SGPR pair is one VALU op and no VGPRs.
+#ifndef MPC_COEF_REG
+#define MPC_COEF_REG "s"   // where Horner coefficients live: "s" SGPR pair, "v" VGPR pair
+#endif
 MPC_HD inline double fma_k(double a, double b, double c) {
 #if defined(__HIP_DEVICE_COMPILE__)
   double r;
-  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), MPC_COEF_REG(c));
   return r;
 #else
   return fma(a, b, c);
@@ -140,25 +143,15 @@ MPC_HD inline double ktan(double x, double y, bool odd) {
   return odd ? cot : th + tl;
 }
 
-// MPC_TRIG_NO_FALLBACK: instruction-count builds only (tools), drops the
-// large-argument branch.
-MPC_HD inline double tan_fast(double x) {
-#ifndef MPC_TRIG_NO_FALLBACK
-  if (!(fabs(x) <= kFastMax)) return ::tan(x);  // huge or NaN
-#endif
+// Core forms: valid for |x| <= kFastMax only (the caller guarantees it or
+// flags the argument as irregular and recomputes with the full forms below).
+MPC_HD inline double tan_core(double x) {
   const Reduced r = reduce_pio2(x);
   const double t = ktan(r.hi, r.lo, (r.q & 1) != 0);
   return x == 0.0 ? x : t;  // tan(+-0) = +-0
 }
 
-MPC_HD inline void sincos_fast(double x, double* s, double* c) {
-#ifndef MPC_TRIG_NO_FALLBACK
-  if (!(fabs(x) <= kFastMax)) {
-    *s = ::sin(x);
-    *c = ::cos(x);
-    return;
-  }
-#endif
+MPC_HD inline void sincos_core(double x, double* s, double* c) {
   const Reduced r = reduce_pio2(x);
   const double sn = ksin(r.hi, r.lo);
   const double cs = kcos(r.hi, r.lo);
@@ -169,6 +162,53 @@ MPC_HD inline void sincos_fast(double x, double* s, double* c) {
   if ((q + 1) & 2) C = -C;
   *s = S;
   *c = C;
+}
+
+// Full forms: any argument (huge or non-finite ones go to the library).
+MPC_HD inline double tan_fast(double x) {
+  if (!(fabs(x) <= kFastMax)) return ::tan(x);
+  return tan_core(x);
+}
+
+MPC_HD inline void sincos_fast(double x, double* s, double* c) {
+  if (!(fabs(x) <= kFastMax)) {
+    *s = ::sin(x);
+    *c = ::cos(x);
+    return;
+  }
+  sincos_core(x, s, c);
+}
+
+// ---------------------------------------------------------------------------
+// Heading rotation (MPC_HEADING_ROTATE mode).  The heading advances by a small
+// increment each step (|dphi| <= |v/L * tan(beta) * dt|, 0.18 rad in the
+// reference's domain), so (sin phi, cos phi) can be carried along the
+// rollout and rotated by dphi instead of re-evaluated with a full range
+// reduction:  s' = s + (s*cm1 + c*sd),  c' = c + (c*cm1 - s*sd)  with
+// sd = sin(dphi), cm1 = cos(dphi) - 1 from short polynomials on |d| <= 0.25
+// (tools/fit_trig.py --small).
+constexpr double kRotMax = 0.25;
+// sin(d) = d + d^3 * RS(d^2);  RS[4] = -1/6
+constexpr double kRS[5] = {-0x1.adf608c9a6f5dp-26, 0x1.71de2e4566711p-19, -0x1.a01a019f064f2p-13,
+                           0x1.1111111111087p-7, -0x1.5555555555555p-3};
+// cos(d) - 1 = -d^2/2 + d^4 * RC(d^2);  RC[4] = 1/24
+constexpr double kRC[5] = {0x1.1eae86305182cp-29, -0x1.27e4f492d03a7p-22, 0x1.a01a019f7c738p-16,
+                           -0x1.6c16c16c16bc8p-10, 0x1.5555555555555p-5};
+
+// sd = sin(d), cm1 = cos(d) - 1 for |d| <= kRotMax (larger increments make
+// the candidate irregular: it is recomputed with direct evaluation)
+MPC_HD inline void rotation_factors(double d, double& sd, double& cm1) {
+  const double z = d * d;
+  sd = fma(d * z, horner(kRS, z), d);
+  cm1 = fma(z * z, horner(kRC, z), -0.5 * z);
+}
+
+// (s, c) <- rotation of (s, c) by the angle whose factors are (sd, cm1)
+MPC_HD inline void rotate_by(double sd, double cm1, double& s, double& c) {
+  const double s1 = s + fma(c, sd, s * cm1);
+  const double c1 = c + fma(-s, sd, c * cm1);
+  s = s1;
+  c = c1;
 }
 
 }  // namespace trig

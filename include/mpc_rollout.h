@@ -45,6 +45,14 @@ enum {
  * RECT: the exact integral f*(t_b - t_a) of the constant integrand.        */
 enum { MPC_INTEG_QK21 = 0, MPC_INTEG_RECT = 1 };
 
+/* Flag OR'ed into every `integrator` argument: carry (sin, cos) of the heading
+ * along the rollout and rotate it by each step's increment dphi instead of
+ * evaluating sin/cos of the new heading (math_model_tree.py:113-114) with a
+ * full range reduction.  Same mathematics, different rounding (a few ulp on
+ * the heading's sin/cos after N steps); ~40% fewer VALU instructions per
+ * candidate-step.  Increments |dphi| > 0.25 fall back to direct evaluation. */
+#define MPC_HEADING_ROTATE 0x100
+
 /* One MPC problem (one robot at one MPC step). */
 typedef struct mpc_problem {
   double x, y, phi;   /* initial_coordinates, math_model_tree.py:294            */

@@ -25,20 +25,25 @@ extern "C" int replica_rollout(const mpc_problem_t* p, const double* v, const do
   K.inv_L = K.L_pow2 ? 1.0 / p->L : 0.0;
   K.h = p->t_b - p->t_a;
   K.hlgth = 0.5 * (p->t_b - p->t_a);
+  double (*volatile sn)(double) = sin;
+  double (*volatile cs)(double) = cos;
+  K.s0 = sn(p->phi);
+  K.c0 = cs(p->phi);
+  const bool rot = (integ & MPC_HEADING_ROTATE) != 0;
+  const int ig = integ & 0xff;
+  double traj[3 * MPC_MAX_STEPS];
   for (int64_t c = 0; c < n_cand; ++c) {
-    double x = K.x, y = K.y, ph = K.phi;
-    for (int s = 0; s < n_steps; ++s) {
-      if (integ == MPC_INTEG_RECT)
-        mpc::step<MPC_INTEG_RECT>(x, y, ph, v[s * n_cand + c], b[s * n_cand + c], K);
-      else
-        mpc::step<MPC_INTEG_QK21>(x, y, ph, v[s * n_cand + c], b[s * n_cand + c], K);
-      if (states) {
-        states[(s * 3 + 0) * n_cand + c] = x;
-        states[(s * 3 + 1) * n_cand + c] = y;
-        states[(s * 3 + 2) * n_cand + c] = ph;
-      }
-    }
-    if (costs) costs[c] = mpc::cost(x, y, K);
+    double cst;
+    if (ig == MPC_INTEG_RECT)
+      cst = rot ? mpc::rollout_candidate<MPC_INTEG_RECT, true>(K, v, b, n_cand, c, n_steps, traj)
+                : mpc::rollout_candidate<MPC_INTEG_RECT, false>(K, v, b, n_cand, c, n_steps, traj);
+    else
+      cst = rot ? mpc::rollout_candidate<MPC_INTEG_QK21, true>(K, v, b, n_cand, c, n_steps, traj)
+                : mpc::rollout_candidate<MPC_INTEG_QK21, false>(K, v, b, n_cand, c, n_steps, traj);
+    if (states)
+      for (int s = 0; s < n_steps; ++s)
+        for (int k = 0; k < 3; ++k) states[(s * 3 + k) * n_cand + c] = traj[3 * s + k];
+    if (costs) costs[c] = cst;
   }
   return 0;
 }

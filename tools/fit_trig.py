@@ -63,5 +63,33 @@ def main():
               ", ".join(c.hex() for c in coeffs) + "};")
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--small" not in __import__("sys").argv:
     main()
+
+
+def fit_small(rmax=0.25, deg_s=4, deg_c=4):
+    """Small-angle sin/cos for the heading rotation recurrence (|d| <= rmax):
+        sin(d) = d + d^3 * Ps(d^2),  cos(d) - 1 = -d^2/2 + d^4 * Pc(d^2)."""
+    smax = mp.mpf(rmax) ** 2
+
+    def Ps(s):
+        if s == 0:
+            return -mp.mpf(1) / 6
+        r = mp.sqrt(s)
+        return (mp.sin(r) - r) / (r * s)
+
+    def Pc(s):
+        if s == 0:
+            return mp.mpf(1) / 24
+        r = mp.sqrt(s)
+        return (mp.cos(r) - 1 + s / 2) / (s * s)
+
+    for name, fn, deg in (("RS", Ps, deg_s), ("RC", Pc, deg_c)):
+        poly, err = mp.chebyfit(fn, [0, smax], deg + 1, error=True)
+        print(f"// {name}: degree {deg} in d^2 on |d| <= {rmax}, fit error {mp.nstr(err, 5)}")
+        print(f"constexpr double k{name}[{deg + 1}] = {{" +
+              ", ".join(d(c).hex() for c in poly) + "};")
+
+
+if __name__ == "__main__" and "--small" in __import__("sys").argv:
+    fit_small()

@@ -101,9 +101,11 @@ def main():
     emit(check="device", name=torch.cuda.get_device_name(0),
          lib=os.environ.get("DIPLOMJOURNEY_MPC_LIB", "in-tree"))
     if "--time-only" in sys.argv:
-        for n_steps, integ in ((10, "rect"), (10, "qk21"), (3, "rect"), (12, "rect")):
+        for n_steps, integ in ((10, "rect"), (10, "rect+rot"), (10, "qk21"), (10, "qk21+rot"),
+                               (3, "rect"), (3, "rect+rot"), (12, "rect"), (12, "rect+rot")):
             time_kernel(eng, 1_000_000, n_steps, integ)
         time_kernel(eng, 8_000_000, 10, "rect")
+        time_kernel(eng, 8_000_000, 10, "rect+rot")
         return
     for n_steps, integ in ((10, "rect"), (10, "qk21"), (3, "rect"), (12, "rect"), (11, "rect"), (8, "rect")):
         time_kernel(eng, 1_000_000, n_steps, integ)
