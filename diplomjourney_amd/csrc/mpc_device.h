@@ -56,12 +56,35 @@ MPC_HD __forceinline__ double quad_const(double f, const Consts& K) {
   }
 }
 
+// The three integrals of one step.  QK21: the reference's quad() (bitwise
+// dqk21 on the constant integrand).  RECT: the same integrals of the constant
+// integrands evaluated directly, h * f, with one rounding fewer per position
+// update: dphi = ((v/L) * h) * tan(beta), x' = fma(v * h, cos phi', x).  (For
+// L a power of two (v * inv_L) * h == (v * h) * inv_L exactly, so both forms of
+// v/L give the same dphi.)
+template <int INTEG>
+MPC_HD __forceinline__ double heading_incr(double w, double t, const Consts& K) {
+  if constexpr (INTEG == MPC_INTEG_RECT)
+    return (w * K.h) * t;
+  else
+    return quad_const<INTEG>(w * t, K);
+}
+
+template <int INTEG>
+MPC_HD __forceinline__ double position_step(double p, double v, double trig, const Consts& K) {
+  if constexpr (INTEG == MPC_INTEG_RECT)
+    return fma(v * K.h, trig, p);
+  else
+    return p + quad_const<INTEG>(v * trig, K);
+}
+
 // iteration_of_predict (math_model_tree.py:111-115): heading first, then
 // position with the updated heading (semi-implicit bicycle step).
 //
 // step_core is the hot-loop form.  It uses the range-limited trig cores and
-// flags the candidate `bad` when an argument leaves their range (|beta| or,
-// in direct mode, |phi| > kFastMax; in rotation mode |dphi| > kRotMax; NaN).
+// flags the candidate `bad` when an argument leaves their range (|beta| >
+// kTanMax; in direct mode |phi| > kFastMax; in rotation mode |dphi| > kRotMax;
+// NaN).
 // A bad candidate is recomputed with step_safe (direct sin/cos, library
 // fallbacks), so every candidate gets a well-defined, correct result while the
 // hot loop carries no fallback code.
@@ -69,12 +92,16 @@ MPC_HD __forceinline__ double quad_const(double f, const Consts& K) {
 //                formula, :113-114)
 //   ROT = true:  (s, c) carry sin/cos of the heading and are rotated by the
 //                increment (mpc_trig.h rotation_factors / rotate_by)
-template <int INTEG, bool ROT>
+//   PL2:         L is a power of two (v / L == v * inv_L exactly).  A template
+//                parameter, not a branch: a branch inside the step would split
+//                the loop into basic blocks and stop the scheduler from
+//                interleaving the lane's independent candidate chains.
+template <int INTEG, bool ROT, bool PL2>
 MPC_HD __forceinline__ void step_core(double& x, double& y, double& ph, double& s, double& c,
                                       double v, double beta, const Consts& K, bool& bad) {
-  bad |= !(fabs(beta) <= trig::kFastMax);
-  const double w = K.L_pow2 ? v * K.inv_L : v / K.L;          // _velocity / L   (:78)
-  const double dphi = quad_const<INTEG>(w * trig::tan_core(beta), K);  // angle_phi (:107)
+  bad |= !(fabs(beta) <= trig::kTanMax);
+  const double w = PL2 ? v * K.inv_L : v / K.L;                // _velocity / L   (:78)
+  const double dphi = heading_incr<INTEG>(w, trig::tan_small(beta), K);  // angle_phi (:107)
   ph = ph + dphi;                                              // phi + _phi      (:113)
   if constexpr (ROT) {
     bad |= !(fabs(dphi) <= trig::kRotMax);
@@ -85,20 +112,20 @@ MPC_HD __forceinline__ void step_core(double& x, double& y, double& ph, double& 
     bad |= !(fabs(ph) <= trig::kFastMax);
     trig::sincos_core(ph, &s, &c);
   }
-  x = x + quad_const<INTEG>(v * c, K);                         // coordinate_x    (:99)
-  y = y + quad_const<INTEG>(v * s, K);                         // coordinate_y    (:103)
+  x = position_step<INTEG>(x, v, c, K);                        // coordinate_x    (:99)
+  y = position_step<INTEG>(y, v, s, K);                        // coordinate_y    (:103)
 }
 
 template <int INTEG>
 MPC_HD __forceinline__ void step_safe(double& x, double& y, double& ph, double v, double beta,
                                       const Consts& K) {
   const double w = K.L_pow2 ? v * K.inv_L : v / K.L;
-  const double dphi = quad_const<INTEG>(w * trig::tan_fast(beta), K);
+  const double dphi = heading_incr<INTEG>(w, trig::tan_fast(beta), K);
   ph = ph + dphi;
   double s, c;
   trig::sincos_fast(ph, &s, &c);
-  x = x + quad_const<INTEG>(v * c, K);
-  y = y + quad_const<INTEG>(v * s, K);
+  x = position_step<INTEG>(x, v, c, K);
+  y = position_step<INTEG>(y, v, s, K);
 }
 
 // control_criterion (math_model_tree.py:82-87) on the layer-N state.
@@ -118,13 +145,13 @@ MPC_HD __forceinline__ double cost(double x, double y, const Consts& K) {
 // tests/replica_harness.cpp calls this): the core recurrence, and if that
 // flags the candidate, the safe recurrence.  traj (optional) gets the
 // per-step (x, y, phi).  Returns the cost.
-template <int INTEG, bool ROT>
-MPC_HD inline double rollout_candidate(const Consts& K, const double* v, const double* b,
-                                       int64_t ld, int64_t col, int n_steps, double* traj) {
+template <int INTEG, bool ROT, bool PL2>
+MPC_HD inline double rollout_candidate_l(const Consts& K, const double* v, const double* b,
+                                         int64_t ld, int64_t col, int n_steps, double* traj) {
   double x = K.x, y = K.y, ph = K.phi, s = K.s0, c = K.c0;
   bool bad = false;
   for (int st = 0; st < n_steps; ++st) {
-    step_core<INTEG, ROT>(x, y, ph, s, c, v[st * ld + col], b[st * ld + col], K, bad);
+    step_core<INTEG, ROT, PL2>(x, y, ph, s, c, v[st * ld + col], b[st * ld + col], K, bad);
     if (traj) {
       traj[3 * st + 0] = x;
       traj[3 * st + 1] = y;
@@ -145,6 +172,13 @@ MPC_HD inline double rollout_candidate(const Consts& K, const double* v, const d
     }
   }
   return cost(x, y, K);
+}
+
+template <int INTEG, bool ROT>
+MPC_HD inline double rollout_candidate(const Consts& K, const double* v, const double* b,
+                                       int64_t ld, int64_t col, int n_steps, double* traj) {
+  return K.L_pow2 ? rollout_candidate_l<INTEG, ROT, true>(K, v, b, ld, col, n_steps, traj)
+                  : rollout_candidate_l<INTEG, ROT, false>(K, v, b, ld, col, n_steps, traj);
 }
 
 // Total order on costs for the arg-min: non-finite costs (NaN, +inf) map to

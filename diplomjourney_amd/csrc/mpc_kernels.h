@@ -2,10 +2,11 @@
 //
 //   k_rollout_argmin   one lane per CPL adjacent candidates (CPL = 2: every
 //                      control load is 16 B per lane = 1 KiB per wave
-//                      instruction); N-step rollout in registers with the next
-//                      step's controls in flight; terminal cost; lane -> wave
-//                      (shuffle) -> block (LDS) lexicographic (cost, index)
-//                      arg-min; one 16-B record per block.
+//                      instruction); N-step rollout in registers with the
+//                      controls of the next kPrefetch-1 steps in flight;
+//                      terminal cost; lane -> wave (shuffle) -> block (LDS)
+//                      lexicographic (cost, index) arg-min; one 16-B record
+//                      per block.
 //   k_finalize         arg-min over the block records; the winner re-rolled
 //                      lane-parallel (bitwise the arithmetic the lane scored).
 //   k_rollout_argmin_batched / k_finalize_batched   robot-segmented variant.
@@ -31,11 +32,22 @@ constexpr int kBlock = 256;  // 4 waves of 64
 #ifndef MPC_CPL
 #define MPC_CPL 2            // candidates per lane on the aligned path (2 or 4)
 #endif
+#ifndef MPC_PREFETCH
+#define MPC_PREFETCH 2       // control-load pipeline depth in steps (>= 2)
+#endif
+#ifndef MPC_GLDS
+#define MPC_GLDS 1           // wide path: LDS-DMA control ring (0: register ring)
+#endif
+#ifndef MPC_EXPERIMENT
+#define MPC_EXPERIMENT 0     // A/B probes only: 1 = loads without the step math, 2 = math without loads
+#endif
 #ifndef MPC_MIN_WAVES
 #define MPC_MIN_WAVES 1      // __launch_bounds__ minimum waves per SIMD
 #endif
 constexpr int kCplWide = MPC_CPL;
 static_assert(kCplWide == 2 || kCplWide == 4, "MPC_CPL must be 2 or 4");
+constexpr int kPrefetch = MPC_PREFETCH;
+static_assert(kPrefetch >= 2, "MPC_PREFETCH must be >= 2");
 constexpr int kWaves = kBlock / 64;
 constexpr int64_t kMaxBlocks = 2048;  // 256 CUs x 8 resident blocks upper bound
 constexpr int kFinBlock = 1024;
@@ -68,8 +80,8 @@ __device__ __forceinline__ void block_argmin(uint64_t& k, int64_t& i) {
 }
 
 // Rollout of CPL adjacent candidates starting at column c0; costs in cst.
-template <int CPL, int INTEG, bool ROT, bool STATES>
-__device__ __forceinline__ void rollout_lane(const Consts& K, const double* __restrict__ v,
+template <int CPL, int INTEG, bool ROT, bool STATES, bool PL2>
+__device__ __forceinline__ void rollout_lane_l(const Consts& K, const double* __restrict__ v,
                                              const double* __restrict__ b, int64_t ld, int64_t c0,
                                              int n_steps, double (&cst)[CPL],
                                              double* __restrict__ states, int64_t n_cand) {
@@ -85,6 +97,14 @@ __device__ __forceinline__ void rollout_lane(const Consts& K, const double* __re
   // Controls of step sr for this lane's CPL candidates: 16 B per lane per
   // array on the wide path (one 1 KiB wave-instruction each).
   auto load = [&](int sr, double (&vv)[CPL], double (&bb)[CPL]) {
+#if MPC_EXPERIMENT == 2
+#pragma unroll
+    for (int h = 0; h < CPL; ++h) {
+      vv[h] = 0.5 + 1e-3 * static_cast<double>((c0 + h + sr) & 15);
+      bb[h] = 0.01 * static_cast<double>(((c0 + h) >> 4) & 31) - 0.15;
+    }
+    return;
+#endif
     if constexpr (CPL >= 2) {
 #pragma unroll
       for (int h = 0; h < CPL; h += 2) {
@@ -106,7 +126,12 @@ __device__ __forceinline__ void rollout_lane(const Consts& K, const double* __re
   auto body = [&](int sr, const double (&vv)[CPL], const double (&bb)[CPL]) {
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
-      step_core<INTEG, ROT>(x[j], y[j], ph[j], sn[j], cs[j], vv[j], bb[j], K, bad[j]);
+#if MPC_EXPERIMENT == 1
+      x[j] = x[j] + vv[j] * bb[j];
+      y[j] = y[j] + vv[j];
+      continue;
+#endif
+      step_core<INTEG, ROT, PL2>(x[j], y[j], ph[j], sn[j], cs[j], vv[j], bb[j], K, bad[j]);
       if constexpr (STATES) {
         states[(sr * 3 + 0) * n_cand + c0 + j] = x[j];
         states[(sr * 3 + 1) * n_cand + c0 + j] = y[j];
@@ -114,18 +139,25 @@ __device__ __forceinline__ void rollout_lane(const Consts& K, const double* __re
       }
     }
   };
-  // Software pipeline, two steps per trip (ping-pong registers, no copies):
-  // the next step's controls are in flight while this step's trig chain runs
-  // (the HBM latency is about one step of VALU work).
-  double va[CPL], ba[CPL], vb[CPL], bb_[CPL];
-  load(0, va, ba);
+  // Software pipeline: the controls of the next kPrefetch-1 steps are in
+  // flight while this step's trig chain runs (rotating register buffers,
+  // kPrefetch steps per trip, static indices, no copies).  One step of VALU
+  // work is far shorter than the loaded HBM latency, so one step of lookahead
+  // leaves the loop waiting on memory.
+  constexpr int D = kPrefetch;
+  double vq[D][CPL], bq[D][CPL];
+#pragma unroll
+  for (int u = 0; u < D - 1; ++u)
+    if (u < n_steps) load(u, vq[u], bq[u]);
 #pragma unroll 1
-  for (int s = 0; s < n_steps; s += 2) {
-    if (s + 1 < n_steps) load(s + 1, vb, bb_);
-    body(s, va, ba);
-    if (s + 1 < n_steps) {
-      if (s + 2 < n_steps) load(s + 2, va, ba);
-      body(s + 1, vb, bb_);
+  for (int s = 0; s < n_steps; s += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int st = s + u;
+      if (st < n_steps) {
+        if (st + D - 1 < n_steps) load(st + D - 1, vq[(u + D - 1) % D], bq[(u + D - 1) % D]);
+        body(st, vq[u], bq[u]);
+      }
     }
   }
   // Irregular candidates (argument outside the trig cores' range, or NaN):
@@ -150,12 +182,157 @@ __device__ __forceinline__ void rollout_lane(const Consts& K, const double* __re
   }
 }
 
+// ---------------------------------------------------------------------------
+// Wide path with an LDS-DMA control ring.  Each wave streams its own 128
+// candidates: per step one global_load_lds_dwordx4 for v and one for beta
+// (1 KiB each, lane-linear: lane l's 16 B land at slot + 16*l) into a ring of
+// kRing step slots per wave, kRing-1 steps ahead of the step being computed.
+// The loads need no VGPRs while in flight (the register ring of rollout_lane_l
+// holds 8 per step of lookahead), so the lookahead is deeper at a lower VGPR
+// count.  The DMA is issued by inline asm, which hipcc neither counts nor
+// orders against the LDS reads: the waits are explicit (vmcnt for "slot
+// landed", lgkmcnt(0) before a slot is refilled) and every asm statement
+// clobbers memory.
+#ifndef MPC_RING
+#define MPC_RING 3           // LDS ring depth in steps (kRing-1 steps in flight)
+#endif
+constexpr int kRing = MPC_RING;
+static_assert(kRing >= 2 && kRing <= 8, "MPC_RING must be in [2, 8]");
+
+// One ring for every instantiation (namespace scope: allocated once per kernel).
+__shared__ double2 g_ring[kWaves][kRing][2][64];  // [wave][slot][v|beta][lane]
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p));
+}
+
+// Both control rows of one step into LDS (v at dst_v, beta at dst_v + 1 KiB).
+__device__ __forceinline__ void glds_step(const double* gv, const double* gb, uint32_t dst_v) {
+  uint32_t keep;
+  asm volatile(
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_add_u32 m0, %3, 0x400\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gv), "v"(gb), "s"(dst_v)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  if constexpr (N == 0)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2)
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6)
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 10)
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if constexpr (N == 12)
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+}
+
+template <int INTEG, bool ROT, bool PL2>
+__device__ __forceinline__ void rollout_lane_glds(const Consts& K, const double* __restrict__ v,
+                                                  const double* __restrict__ b, int64_t ld,
+                                                  int64_t c0, int n_steps, double (&cst)[2]) {
+  constexpr int CPL = 2;
+  constexpr int R = kRing;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t ring0 = __builtin_amdgcn_readfirstlane(lds_addr(&g_ring[wv][0][0][0]));
+  constexpr uint32_t kSlot = 2 * 64 * sizeof(double2);  // 2 KiB
+  auto issue = [&](int sr, int slot) {
+    glds_step(v + sr * ld + c0, b + sr * ld + c0, ring0 + slot * kSlot);
+  };
+  double x[CPL], y[CPL], ph[CPL], sn[CPL], cs[CPL];
+  bool bad[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    x[j] = K.x;
+    y[j] = K.y;
+    ph[j] = K.phi;
+    sn[j] = K.s0;
+    cs[j] = K.c0;
+    bad[j] = false;
+  }
+#pragma unroll
+  for (int u = 0; u < R - 1; ++u)
+    if (u < n_steps) issue(u, u);
+#pragma unroll 1
+  for (int s = 0; s < n_steps; s += R) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int st = s + u;
+      if (st < n_steps) {
+        if (st + R - 1 < n_steps) {
+          issue(st + R - 1, (u + R - 1) % R);
+          wait_vm<2 * (R - 1)>();   // this step's pair has landed
+        } else {
+          wait_vm<0>();             // pipeline tail
+        }
+        const double2 v2 = g_ring[wv][u][0][lane];
+        const double2 b2 = g_ring[wv][u][1][lane];
+        step_core<INTEG, ROT, PL2>(x[0], y[0], ph[0], sn[0], cs[0], v2.x, b2.x, K, bad[0]);
+        step_core<INTEG, ROT, PL2>(x[1], y[1], ph[1], sn[1], cs[1], v2.y, b2.y, K, bad[1]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    if (bad[j]) {
+      x[j] = K.x;
+      y[j] = K.y;
+      ph[j] = K.phi;
+      for (int sr = 0; sr < n_steps; ++sr)
+        step_safe<INTEG>(x[j], y[j], ph[j], v[sr * ld + c0 + j], b[sr * ld + c0 + j], K);
+    }
+    cst[j] = cost(x[j], y[j], K);
+  }
+}
+
+// L a power of two or not: one loop body each (see step_core).
+template <int CPL, int INTEG, bool ROT, bool STATES>
+__device__ __forceinline__ void rollout_lane(const Consts& K, const double* __restrict__ v,
+                                             const double* __restrict__ b, int64_t ld, int64_t c0,
+                                             int n_steps, double (&cst)[CPL],
+                                             double* __restrict__ states, int64_t n_cand) {
+#if MPC_GLDS
+  if constexpr (CPL == 2 && !STATES) {
+    if (K.L_pow2)
+      rollout_lane_glds<INTEG, ROT, true>(K, v, b, ld, c0, n_steps, cst);
+    else
+      rollout_lane_glds<INTEG, ROT, false>(K, v, b, ld, c0, n_steps, cst);
+    return;
+  }
+#endif
+  if (K.L_pow2)
+    rollout_lane_l<CPL, INTEG, ROT, STATES, true>(K, v, b, ld, c0, n_steps, cst, states, n_cand);
+  else
+    rollout_lane_l<CPL, INTEG, ROT, STATES, false>(K, v, b, ld, c0, n_steps, cst, states, n_cand);
+}
+
 template <int CPL, int INTEG, bool ROT, bool STATES, bool KDEV>
 __global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(
     Consts Karg, const Consts* __restrict__ Kdev, const double* __restrict__ v,
-    const double* __restrict__ b, int64_t n_cand, int n_steps, int64_t n_tiles,
-    Rec* __restrict__ part, double* __restrict__ states) {
+    const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part,
+    double* __restrict__ states) {
   const Consts K = KDEV ? *Kdev : Karg;
+  const int64_t n_tiles = (n_cand + kBlock * CPL - 1) / (kBlock * CPL);
   uint64_t best_k = ~0ull;
   int64_t best_i = INT64_MAX;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
@@ -208,15 +385,19 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
   col = s_col;
   const int lane = threadIdx.x;
   const bool valid = key != ~0ull;
+  // Regular pass (step_core's forms and range checks), then — if any step is
+  // irregular — the safe pass (step_safe's forms) for the whole candidate,
+  // exactly as rollout_candidate / the rollout kernels decide.
+  double vs = 0.0, w = 0.0, bs = 0.0;
   if (valid && lane < n_steps) {
-    const double vs = v[lane * ld + col];
-    const double bs = b[lane * ld + col];
+    vs = v[lane * ld + col];
+    bs = b[lane * ld + col];
     s_v[lane] = vs;
     if (lane == 0) s_b0 = bs;
-    const double w = K.L_pow2 ? vs * K.inv_L : vs / K.L;
-    const double d = quad_const<INTEG>(w * trig::tan_fast(bs), K);  // == tan_core if regular
+    w = K.L_pow2 ? vs * K.inv_L : vs / K.L;
+    const double d = heading_incr<INTEG>(w, trig::tan_small(bs), K);
     s_dphi[lane] = d;
-    if (!(fabs(bs) <= trig::kFastMax) || (ROT && !(fabs(d) <= trig::kRotMax))) s_bad = 1;
+    if (!(fabs(bs) <= trig::kTanMax) || (ROT && !(fabs(d) <= trig::kRotMax))) s_bad = 1;
   }
   __syncthreads();
   if (valid && lane == 0) {
@@ -228,6 +409,18 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
     }
   }
   __syncthreads();
+  if (s_bad) {
+    if (valid && lane < n_steps) s_dphi[lane] = heading_incr<INTEG>(w, trig::tan_fast(bs), K);
+    __syncthreads();
+    if (valid && lane == 0) {
+      double ph = K.phi;
+      for (int st = 0; st < n_steps; ++st) {
+        ph = ph + s_dphi[st];
+        s_phi[st] = ph;
+      }
+    }
+    __syncthreads();
+  }
   const bool bad = s_bad != 0;
   if (valid && lane < n_steps) {
     if (ROT && !bad)
@@ -260,8 +453,8 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
       sn = s_a[st];
       cs = s_c[st];
     }
-    x = x + quad_const<INTEG>(s_v[st] * cs, K);
-    y = y + quad_const<INTEG>(s_v[st] * sn, K);
+    x = position_step<INTEG>(x, s_v[st], cs, K);
+    y = position_step<INTEG>(y, s_v[st], sn, K);
     out->traj[st][0] = x;
     out->traj[st][1] = y;
     out->traj[st][2] = s_phi[st];

@@ -59,7 +59,7 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 inline int64_t rollout_blocks(int64_t n_cand) {
-  // CPL=1 tiling has the most tiles; the workspace is sized for it.
+  // Upper bound on the rollout grid (the workspace is sized for it).
   return std::max<int64_t>(1, std::min<int64_t>(cdiv(n_cand, kBlock), kMaxBlocks));
 }
 
@@ -69,11 +69,11 @@ bool wide_ok(const double* v_sc, const double* beta_sc, int64_t n) {
   return (n % kCplWide == 0) && aligned16(v_sc) && aligned16(beta_sc);
 }
 
-int64_t partial_count(const double* v_sc, const double* beta_sc, int64_t n_cand,
-                      bool with_states) {
-  const bool wide = !with_states && wide_ok(v_sc, beta_sc, n_cand);
-  const int64_t tiles = cdiv(n_cand, kBlock * (wide ? kCplWide : 1));
-  return std::min<int64_t>(tiles, kMaxBlocks);
+// Tile-strided grid: one block per tile of kBlock*CPL candidates, at most
+// kMaxBlocks (blocks then stride over the tiles).
+template <int CPL>
+int64_t rollout_grid(int64_t n_cand) {
+  return std::max<int64_t>(1, std::min<int64_t>(cdiv(n_cand, kBlock * CPL), kMaxBlocks));
 }
 
 template <int V>
@@ -100,22 +100,30 @@ void dispatch_mode(int32_t integrator, F&& f) {
   }
 }
 
+// Number of block records the rollout launch for these arguments writes
+// (= its grid); the finalize launch reduces exactly these.
+int64_t partial_count(const double* v_sc, const double* beta_sc, int64_t n_cand,
+                      bool with_states) {
+  const bool wide = !with_states && wide_ok(v_sc, beta_sc, n_cand);
+  return wide ? rollout_grid<kCplWide>(n_cand) : rollout_grid<1>(n_cand);
+}
+
 // The streaming kernel: wide (CPL = kCplWide) or scalar path.
 template <bool KDEV>
 void launch_rollout(hipStream_t st, int32_t integrator, const Consts& K, const Consts* Kdev,
                     const double* v, const double* b, int64_t n_cand, int n_steps, Rec* part) {
   const bool wide = wide_ok(v, b, n_cand);
-  const int64_t tiles = cdiv(n_cand, kBlock * (wide ? kCplWide : 1));
-  const int64_t grid = std::min<int64_t>(tiles, kMaxBlocks);
   dispatch_mode(integrator, [&](auto integ, auto rot) {
     constexpr int I = decltype(integ)::value;
     constexpr bool R = decltype(rot)::value;
     if (wide)
       k_rollout_argmin<kCplWide, I, R, false, KDEV>
-          <<<grid, kBlock, 0, st>>>(K, Kdev, v, b, n_cand, n_steps, tiles, part, nullptr);
+          <<<rollout_grid<kCplWide>(n_cand), kBlock, 0, st>>>(
+              K, Kdev, v, b, n_cand, n_steps, part, nullptr);
     else
       k_rollout_argmin<1, I, R, false, KDEV>
-          <<<grid, kBlock, 0, st>>>(K, Kdev, v, b, n_cand, n_steps, tiles, part, nullptr);
+          <<<rollout_grid<1>(n_cand), kBlock, 0, st>>>(
+              K, Kdev, v, b, n_cand, n_steps, part, nullptr);
   });
 }
 
@@ -188,13 +196,12 @@ int mpc_rollout_partials(const mpc_problem_t* p, const double* v_sc, const doubl
   Rec* part = static_cast<Rec*>(ws);
   if (states_out) {
     // CoordinateTree materialisation path: one candidate per lane, all states out.
-    const int64_t tiles = cdiv(n_cand, kBlock);
-    const int64_t grid = std::min<int64_t>(tiles, kMaxBlocks);
     dispatch_mode(integrator, [&](auto integ, auto rot) {
       constexpr int I = decltype(integ)::value;
       constexpr bool R = decltype(rot)::value;
-      k_rollout_argmin<1, I, R, true, false><<<grid, kBlock, 0, st>>>(
-          K, nullptr, v_sc, beta_sc, n_cand, n_steps, tiles, part, states_out);
+      k_rollout_argmin<1, I, R, true, false>
+          <<<rollout_grid<1>(n_cand), kBlock, 0, st>>>(
+              K, nullptr, v_sc, beta_sc, n_cand, n_steps, part, states_out);
     });
   } else {
     launch_rollout<false>(st, integrator, K, nullptr, v_sc, beta_sc, n_cand, n_steps, part);

@@ -143,6 +143,35 @@ MPC_HD inline double ktan(double x, double y, bool odd) {
   return odd ? cot : th + tl;
 }
 
+// Steering-angle tangent without range reduction, |x| <= kTanMax:
+//   tan(x) = x + x^3 * TP(x^2) / TQ(x^2)
+// (tools/fit_trig.py --tan-rational; rel. error of TP/TQ 2.8e-20).  One
+// reciprocal estimate, one Newton step and one correction of the quotient
+// replace the Cody-Waite reduction and the quadrant/cotangent reconstruction
+// of tan_core: ~17 VALU instead of ~50.  The steering bound of the
+// reference's config is 60 deg = 1.047 rad; a larger |beta| makes the
+// candidate irregular (recomputed with tan_fast).
+constexpr double kTanMax = 1.1;
+constexpr double kTP[4] = {-0x1.5a006cab24f4bp-20, 0x1.88ebe003d6902p-12, -0x1.81d5aba9c1240p-6,
+                           0x1.5555555555555p-2};
+constexpr double kTQ[5] = {0x1.61e9925b7b933p-20, -0x1.a739351555585p-12, 0x1.c2364f9313e10p-6,
+                           -0x1.e1f1a9c96dd06p-2, 0x1.0000000000000p+0};
+
+MPC_HD inline double tan_small(double x) {
+  const double s = x * x;
+  const double p = horner(kTP, s);
+  const double q = horner(kTQ, s);        // in [0.59, 1]
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r = __builtin_amdgcn_rcp(q);
+#else
+  double r = 1.0 / q;
+#endif
+  r = fma(r, fma(-q, r, 1.0), r);
+  double R = p * r;
+  R = fma(r, fma(-q, R, p), R);           // quotient correction
+  return fma(x * s, R, x);
+}
+
 // Core forms: valid for |x| <= kFastMax only (the caller guarantees it or
 // flags the argument as irregular and recomputes with the full forms below).
 MPC_HD inline double tan_core(double x) {
@@ -181,19 +210,20 @@ MPC_HD inline void sincos_fast(double x, double* s, double* c) {
 
 // ---------------------------------------------------------------------------
 // Heading rotation (MPC_HEADING_ROTATE mode).  The heading advances by a small
-// increment each step (|dphi| <= |v/L * tan(beta) * dt|, 0.18 rad in the
-// reference's domain), so (sin phi, cos phi) can be carried along the
+// increment each step (|dphi| <= v_max/L * tan(beta_max) * dt = 0.173 rad in
+// the reference's config), so (sin phi, cos phi) can be carried along the
 // rollout and rotated by dphi instead of re-evaluated with a full range
 // reduction:  s' = s + (s*cm1 + c*sd),  c' = c + (c*cm1 - s*sd)  with
-// sd = sin(dphi), cm1 = cos(dphi) - 1 from short polynomials on |d| <= 0.25
+// sd = sin(dphi), cm1 = cos(dphi) - 1 from short polynomials on |d| <= 0.2
 // (tools/fit_trig.py --small).
-constexpr double kRotMax = 0.25;
-// sin(d) = d + d^3 * RS(d^2);  RS[4] = -1/6
-constexpr double kRS[5] = {-0x1.adf608c9a6f5dp-26, 0x1.71de2e4566711p-19, -0x1.a01a019f064f2p-13,
-                           0x1.1111111111087p-7, -0x1.5555555555555p-3};
-// cos(d) - 1 = -d^2/2 + d^4 * RC(d^2);  RC[4] = 1/24
-constexpr double kRC[5] = {0x1.1eae86305182cp-29, -0x1.27e4f492d03a7p-22, 0x1.a01a019f7c738p-16,
-                           -0x1.6c16c16c16bc8p-10, 0x1.5555555555555p-5};
+constexpr double kRotMax = 0.2;
+// sin(d) = d + d^3 * RS(d^2);  RS[3] ~ -1/6   (near-minimax on |d| <= 0.2; the
+// abs. error of the d^3 term is <= 4e-18, 0.15 ulp of sin(0.2))
+constexpr double kRS[4] = {0x1.719963b18b037p-19, -0x1.a019fabe07951p-13, 0x1.11111110d8aedp-7,
+                           -0x1.5555555555543p-3};
+// cos(d) - 1 = -d^2/2 + d^4 * RC(d^2);  RC[3] ~ 1/24   (abs. error <= 7e-20)
+constexpr double kRC[4] = {-0x1.27b71672cf54cp-22, 0x1.a019fd094f3a7p-16, -0x1.6c16c16bf129ep-10,
+                           0x1.555555555554fp-5};
 
 // sd = sin(d), cm1 = cos(d) - 1 for |d| <= kRotMax (larger increments make
 // the candidate irregular: it is recomputed with direct evaluation)

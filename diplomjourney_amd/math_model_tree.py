@@ -48,7 +48,8 @@ random = np.random
 
 VERBOSE = False
 # Integration rule of the device kernel: "qk21" reproduces sp.quad bit for bit
-# on a constant integrand (the reference's arithmetic); "rect" is f*h.
+# on a constant integrand (the reference's arithmetic); "rect" evaluates the same
+# integrals directly (h*f, positions with one fused rounding; mpc_device.h).
 INTEGRATOR = "qk21"
 
 # Prediction horizon * delta_t = 0.15 s (:27)

@@ -26,6 +26,7 @@ def trig_lib():
     L = _build("trig_harness", ["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC",
                                 "-shared"])
     L.trig_eval.argtypes = [_P, ctypes.c_int64, _P, _P, _P]
+    L.trig_tan_small.argtypes = [_P, ctypes.c_int64, _P]
     return L
 
 
@@ -36,6 +37,13 @@ def trig_eval(x):
     trig_lib().trig_eval(x.ctypes.data_as(_P), n, t.ctypes.data_as(_P), s.ctypes.data_as(_P),
                          c.ctypes.data_as(_P))
     return t, s, c
+
+
+def tan_small(x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    t = np.empty(len(x))
+    trig_lib().trig_tan_small(x.ctypes.data_as(_P), len(x), t.ctypes.data_as(_P))
+    return t
 
 
 def replica_lib():

@@ -8,7 +8,7 @@ import mpmath as mp
 import numpy as np
 import pytest
 
-from harness import trig_eval
+from harness import tan_small, trig_eval
 
 _m = ctypes.CDLL("libm.so.6")
 for _f in ("tan", "sin", "cos"):
@@ -53,3 +53,21 @@ def test_special_values():
         for out, f in ((t, math.tan), (s, math.sin), (c, math.cos)):
             assert abs(out[i] - f(x[i])) <= 2 * np.spacing(abs(f(x[i])))
     assert np.all(np.isnan(t[10:])) and np.all(np.isnan(s[10:])) and np.all(np.isnan(c[10:]))
+
+
+def test_tan_small_accuracy():
+    """The rollout loop's steering tangent (rational, no reduction, |x| <=
+    kTanMax = 1.1): within 2 ulp of the exact value (1.87 measured, 1.3 %
+    of arguments at or above 1 ulp), odd, exact at 0."""
+    mp.mp.prec = 120
+    rng = np.random.default_rng(9)
+    x = np.concatenate([rng.uniform(-1.1, 1.1, 4000), np.linspace(1.0, 1.1, 500),
+                        rng.uniform(-1e-3, 1e-3, 200)])
+    t = tan_small(x)
+    worst = max(_ulp_err(g, xi, mp.tan) for g, xi in zip(t, x))
+    assert worst < 2.0, worst
+    assert np.array_equal(tan_small(-x), -t)
+    z = tan_small(np.array([0.0, -0.0, 5e-324, 1e-300]))
+    assert z[0] == 0.0 and math.copysign(1, z[1]) == -1 and z[2] == 5e-324 and z[3] == 1e-300
+    g = np.array([_m.tan(v) for v in x])
+    assert np.mean(t == g) > 0.8            # ~0.87 measured

@@ -8,3 +8,7 @@ extern "C" void trig_eval(const double* x, int64_t n, double* t, double* s, doub
     mpc::trig::sincos_fast(x[i], &s[i], &c[i]);
   }
 }
+
+extern "C" void trig_tan_small(const double* x, int64_t n, double* t) {
+  for (int64_t i = 0; i < n; ++i) t[i] = mpc::trig::tan_small(x[i]);
+}

@@ -63,11 +63,11 @@ def main():
               ", ".join(c.hex() for c in coeffs) + "};")
 
 
-if __name__ == "__main__" and "--small" not in __import__("sys").argv:
+if __name__ == "__main__" and len(__import__("sys").argv) == 1:
     main()
 
 
-def fit_small(rmax=0.25, deg_s=4, deg_c=4):
+def fit_small(rmax=0.2, deg_s=3, deg_c=3):
     """Small-angle sin/cos for the heading rotation recurrence (|d| <= rmax):
         sin(d) = d + d^3 * Ps(d^2),  cos(d) - 1 = -d^2/2 + d^4 * Pc(d^2)."""
     smax = mp.mpf(rmax) ** 2
@@ -93,3 +93,51 @@ def fit_small(rmax=0.25, deg_s=4, deg_c=4):
 
 if __name__ == "__main__" and "--small" in __import__("sys").argv:
     fit_small()
+
+
+def fit_tan_rational(xmax=1.1, m=3, n=4, iters=40, nodes=240):
+    """Rational tan for the steering angle, no range reduction (|x| <= xmax):
+        tan(x) = x + x^3 * P(x^2) / Q(x^2),   Q(0) = 1.
+    Linearised least squares (Sanathanan-Koerner) with Lawson weights for a
+    near-minimax relative error of P/Q against T(s) = (tan(r) - r) / r^3."""
+    mp.mp.dps = 60
+    smax = mp.mpf(xmax) ** 2
+
+    def T(s):
+        if s == 0:
+            return mp.mpf(1) / 3
+        r = mp.sqrt(s)
+        return (mp.tan(r) - r) / (r * s)
+
+    pts = [smax * (1 - mp.cos(mp.pi * (k + mp.mpf(1) / 2) / nodes)) / 2 for k in range(nodes)]
+    fv = [T(s) for s in pts]
+    w = [mp.mpf(1)] * nodes
+    qprev = [mp.mpf(1)] * nodes
+    for it in range(iters):
+        rows, rhs = [], []
+        for s, f, wi, qp in zip(pts, fv, w, qprev):
+            sc = mp.sqrt(wi) / (qp * f)
+            rows.append([sc * s ** i for i in range(m + 1)] +
+                        [-sc * f * s ** j for j in range(1, n + 1)])
+            rhs.append(sc * f)
+        x = mp.qr_solve(mp.matrix(rows), mp.matrix(rhs))[0]
+        p = [x[i] for i in range(m + 1)]
+        q = [mp.mpf(1)] + [x[m + 1 + j] for j in range(n)]
+
+        def R(s):
+            return mp.polyval(p[::-1], s) / mp.polyval(q[::-1], s)
+
+        err = [(R(s) - f) / f for s, f in zip(pts, fv)]
+        qprev = [mp.polyval(q[::-1], s) for s in pts]
+        if it >= 5:
+            tot = sum(wi * abs(e) for wi, e in zip(w, err))
+            w = [wi * abs(e) / tot * nodes for wi, e in zip(w, err)]
+    worst = max(abs((R(s) - T(s)) / T(s)) for s in (smax * k / 2000 for k in range(2001)))
+    print(f"// tan(x) = x + x^3 * TP(x^2) / TQ(x^2) on |x| <= {xmax}, rel. error of P/Q "
+          f"{mp.nstr(worst, 5)}")
+    print(f"constexpr double kTP[{m + 1}] = {{" + ", ".join(d(c).hex() for c in p[::-1]) + "};")
+    print(f"constexpr double kTQ[{n + 1}] = {{" + ", ".join(d(c).hex() for c in q[::-1]) + "};")
+
+
+if __name__ == "__main__" and "--tan-rational" in __import__("sys").argv:
+    fit_tan_rational()
