@@ -13,13 +13,25 @@ Workloads:
   E            1024 robots x 1e4 candidates, N=8, batched per-robot arg-min,
                robots sharded over GPUs (128 per GPU at 8), no exchange
 
-A "step" is one MPC step: host grid -> device sampler -> rollout kernel ->
-finalize -> [RCCL exchange] -> 808-B winner read -> host episode update.
-Controls never leave HBM; inputs to the timed region are device-resident.
+A "step" is one MPC step of the device-resident episode (state in HBM, no
+host synchronisation inside the loop):
+  --inputs resident (default)  the step's candidate batch is already in HBM
+      (a distinct synthetic batch per step, generated before the timed
+      region): rollout/arg-min kernel -> finalize kernel (winner re-roll +
+      episode update: finishing logic, operator events, next step's problem)
+  --inputs sampled  the device sampler first regenerates the candidates on the
+      grid around the episode's current control (the reference's per-step
+      grid), then the same two kernels
+On G > 1 GPUs the per-rank winners are exchanged with one RCCL all_gather
+before the episode update.  `value` is timed over K steps replayed from a HIP
+graph (one GPU) or launched eagerly (G > 1); p50/p90 come from a separate
+eager pass with HIP events; `other_inputs` repeats the run with the other
+input mode.  --host-loop runs the host-driven episode instead.
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel
 (k_rollout_argmin): algorithmic bytes 16 B per candidate-step (fp64 v and
-beta read once) / its average duration from HIP events on the launch stream.
+beta read once) / its average duration, from HIP events around 20
+back-to-back launches on the episode's stream and controls.
 `cpu_baseline` is the reference-structured Python port (scipy quad) on this
 host's cores, rank 0 at N=1 only, on a bounded sample of the same candidates;
 it runs before the GPU is initialised (it forks worker processes).
@@ -54,12 +66,23 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="C", choices=sorted(WORKLOADS))
-    ap.add_argument("--integrator", default="rect", choices=["rect", "qk21"])
+    ap.add_argument("--integrator", default="rect+rot",
+                    choices=["rect+rot", "rect", "qk21+rot", "qk21"],
+                    help="kernel arithmetic (DESIGN.md 'Integrators'): qk21 = the reference's "
+                         "quad() bit for bit, rect = direct h*f; +rot = heading carried as "
+                         "(sin, cos) and rotated per step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="per-core time budget of the cpu_baseline sample (0 = skip)")
     ap.add_argument("--host-loop", action="store_true",
                     help="drive the episode from the host (one 808-B read + host update per "
                          "step) instead of the device-resident episode")
+    ap.add_argument("--inputs", default="resident", choices=["resident", "sampled"],
+                    help="resident: each step's candidates already in HBM (the contract's "
+                         "input); sampled: the device sampler regenerates them per step")
+    ap.add_argument("--no-second-pass", action="store_true",
+                    help="skip the comparison run with the other --inputs mode")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="time eagerly launched steps instead of a HIP graph replay")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks on fewer GPUs (exchange staged via host)")
     ap.add_argument("--candidates-per-gpu", type=int, default=None,
@@ -120,26 +143,145 @@ def main():
 
     from diplomjourney_amd.episode import DeviceEpisode, Episode, percentile
     n_total = (args.candidates_per_gpu or wl["per_gpu"]) * world
+    n_steps = wl["n_steps"]
+    use_graph = world == 1 and not args.host_loop and not args.no_graph
+    inputs = "sampled" if args.host_loop else args.inputs
     if args.host_loop:
-        ep = Episode(eng, n_total, wl["n_steps"], rank=rank, world=world,
+        ep = Episode(eng, n_total, n_steps, rank=rank, world=world,
                      integrator=args.integrator, group=group)
     else:
-        ep = DeviceEpisode(eng, n_total, wl["n_steps"], rank=rank, world=world,
-                           integrator=args.integrator, group=group,
-                           log_capacity=args.steps + args.warmup)
-    for _ in range(args.warmup):
-        ep.step()
+        ep = DeviceEpisode(eng, n_total, n_steps, rank=rank, world=world,
+                           integrator=args.integrator, group=group, log_capacity=8192)
+    pool = make_pool(eng, ep, n_steps, args.steps) if inputs == "resident" else None
+    main_run = run_steps(args, ep, pool, use_graph, world, device)
+    kern_ms = main_run["kernel_in_step_ms"]
+    if hasattr(ep, "partials"):
+        kern_ms = kernel_pass(ep)
+    other = None
+    if not args.host_loop and not args.no_second_pass:
+        # the other input mode, same episode machinery, for comparison
+        other_pool = None if inputs == "resident" else make_pool(eng, ep, n_steps, args.steps)
+        r = run_steps(args, ep, other_pool, use_graph, world, device)
+        other = {"inputs": "sampled" if inputs == "resident" else "resident",
+                 "value": n_total * args.steps / r["elapsed"],
+                 "ms_per_step": r["elapsed"] / args.steps * 1e3, "p50_ms": r["p50_ms"]}
+        del other_pool
+    elapsed = main_run["elapsed"]
+    bytes_launch = 16.0 * n_steps * ep.n_local
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    value = n_total * args.steps / elapsed
+    if not args.host_loop:
+        log = ep.read_log()
+        if args.dump_log and rank == 0:
+            with open(args.dump_log, "w") as fh:
+                json.dump([{f: getattr(r, f) for f, _ in r._fields_} for r in log], fh)
+        assert len(log) == min(ep.steps_enqueued, ep.log_capacity), (len(log), ep.steps_enqueued)
+        missing = [r.step for r in log if r.index < 0]
+        assert not missing, f"steps without a winner: {missing[:20]}"
+        episodes = log[-1].episode
+    else:
+        episodes = ep.episodes
+    out = {
+        "metric": METRIC, "value": value, "unit": "rollouts/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": wl["desc"], "n_steps": n_steps,
+                   "candidates_per_gpu": ep.n_local, "candidates_total": n_total,
+                   "integrator": args.integrator, "inputs": INPUTS_DOC[inputs],
+                   "episodes_started": episodes,
+                   "episode_loop": "host" if args.host_loop else "device-resident",
+                   "launch": "hipGraph of the K steps" if use_graph else "eager",
+                   "parallelism": f"candidate-sharded x{world}" + (", all_gather(808 B)/step"
+                                                                   if world > 1 else "")},
+        "p50_ms": main_run["p50_ms"], "p90_ms": main_run["p90_ms"],
+        "p50_note": "GPU time per MPC step (HIP events between step starts, eager launches)",
+        "kernel_ms": kern_ms, "kernel_in_step_ms": main_run["kernel_in_step_ms"],
+        "roofline": roofline(achieved, bytes_launch, args.traffic_json),
+        "other_inputs": other,
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+INPUTS_DOC = {
+    "resident": "per step a distinct synthetic candidate batch already in HBM (generated "
+                "before the timed region by the device sampler: reference grid around "
+                "v=0.5, beta=0, const-control prefix); the step = rollout/arg-min + "
+                "finalize/episode update",
+    "sampled": "per step the device sampler regenerates the candidates on the grid around "
+               "the episode's current control (the reference's per-step grid); the step = "
+               "sampler + rollout/arg-min + finalize/episode update",
+}
+
+
+def make_pool(eng, ep, n_steps, k):
+    """Distinct resident candidate batches for the timed steps (cycled when
+    K batches would exceed ~16 GB; at least 4, so a batch is never
+    cache-resident when it comes round again)."""
+    import torch
+    from diplomjourney_amd import math_model_tree as mmt
+    batch = 16 * n_steps * ep.n_local
+    n = max(1, min(k, max(4, int(16e9 // batch))))
+    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device=eng.device)
+    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device=eng.device)
+    pool = [eng.sample_controls(V, B, ep.n_local, n_steps, 0x5EED0000 + i, index_base=ep.lo)
+            for i in range(n)]
+    torch.cuda.synchronize()
+    return pool
+
+
+def run_steps(args, ep, pool, use_graph, world, device):
+    """Warmup, an eager latency pass (events), then the timed K steps."""
+    import torch
+    import torch.distributed as dist
+    from diplomjourney_amd.episode import percentile
+
+    def step(i, events=None):
+        if pool is None:
+            ep.step(events=events)
+        else:
+            ep.step(events=events, controls=pool[i % len(pool)])
+
+    for i in range(args.warmup):
+        step(i)
     Ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     kern = [(Ev(), Ev()) for _ in range(args.steps)]
     marks = [Ev() for _ in range(args.steps + 1)]
+    torch.cuda.synchronize()
+    for i in range(args.steps):
+        marks[i].record()
+        step(i, kern[i])
+    marks[-1].record()
+    torch.cuda.synchronize()
+    step_gpu_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)]
+    # Throughput pass: the K steps captured once into a HIP graph (the episode
+    # lives in HBM, so a replay simply continues it) and replayed: no host
+    # cost between the step's kernels.  Multi-GPU runs launch eagerly (the
+    # RCCL exchange stays outside graph capture).
+    graph = None
+    if use_graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for i in range(args.steps):
+                step(i)
+        ep.steps_enqueued -= args.steps      # captured, not run
+        graph.replay()                       # untimed: first replay
+        ep.steps_enqueued += args.steps
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        marks[i].record()
-        ep.step(events=kern[i])
-    marks[-1].record()
+    if graph is not None:
+        graph.replay()
+        ep.steps_enqueued += args.steps
+    else:
+        for i in range(args.steps):
+            step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -148,41 +290,25 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kern_ms = sum(a.elapsed_time(b) for a, b in kern) / len(kern)
-    step_gpu_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)]
-    bytes_launch = 16.0 * wl["n_steps"] * ep.n_local
-    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    value = n_total * args.steps / elapsed
-    if not args.host_loop:
-        log = ep.read_log()
-        assert len(log) == args.steps + args.warmup and all(r.index >= 0 for r in log)
-        episodes = log[-1].episode
-        if args.dump_log and rank == 0:
-            with open(args.dump_log, "w") as fh:
-                json.dump([{f: getattr(r, f) for f, _ in r._fields_} for r in log], fh)
-    else:
-        episodes = ep.episodes
-    out = {
-        "metric": METRIC, "value": value, "unit": "rollouts/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": wl["desc"], "n_steps": wl["n_steps"],
-                   "candidates_per_gpu": ep.n_local, "candidates_total": n_total,
-                   "integrator": args.integrator, "episodes_started": episodes,
-                   "episode_loop": "host" if args.host_loop else "device-resident",
-                   "parallelism": f"candidate-sharded x{world}" + (", all_gather(808 B)/step"
-                                                                   if world > 1 else "")},
-        "p50_ms": percentile(step_gpu_ms, 50), "p90_ms": percentile(step_gpu_ms, 90),
-        "p50_note": "GPU time per MPC step (HIP events between step starts)",
-        "kernel_ms": kern_ms,
-        "roofline": roofline(achieved, bytes_launch, args.traffic_json),
-        "cpu_baseline": cpu,
-    }
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    return {"elapsed": elapsed, "p50_ms": percentile(step_gpu_ms, 50),
+            "p90_ms": percentile(step_gpu_ms, 90),
+            "kernel_in_step_ms": sum(a.elapsed_time(b) for a, b in kern) / len(kern)}
+
+
+def kernel_pass(ep, reps=20):
+    """The rollout kernel alone: REPS back-to-back launches on the current
+    controls between two HIP events on the launch stream (events around the
+    single launch inside a step add their own packet overhead)."""
+    import torch
+    k0 = torch.cuda.Event(enable_timing=True)
+    k1 = torch.cuda.Event(enable_timing=True)
+    ep.partials()
+    k0.record()
+    for _ in range(reps):
+        ep.partials()
+    k1.record()
+    torch.cuda.synchronize()
+    return k0.elapsed_time(k1) / reps
 
 
 def roofline(achieved, bytes_launch, traffic_json):

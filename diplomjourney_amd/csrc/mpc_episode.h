@@ -4,9 +4,9 @@
 //
 //   k_episode_sample   every block derives this step's grids (:239-256,
 //                      slow-down :312-316) with one wave and samples its
-//                      candidates; block 0 publishes t += dt (:302), the
-//                      problem constants and the seed for the launches that
-//                      follow on the stream
+//                      candidates; block 0 publishes the grids.  (t += dt
+//                      (:302), the step's problem constants and seed are
+//                      prepared by reset / the previous advance.)
 //   k_finalize<..., KDEV> + episode_hook   (one GPU) winner -> episode update
 //   k_episode_advance  (multi-GPU) selection over the gathered per-rank
 //                      winners, then the episode update
@@ -21,21 +21,16 @@ namespace mpc {
 
 constexpr int kEpMaxGrid = 64;
 
+// EpisodeHead (mpc_kernels.h): the scalars; the grids only feed the sampler.
 struct EpisodeState {
-  Consts K;            // this step's problem constants
-  double incumbent;    // optimal_criterion at the start of this step
-  double x, y, phi, v, beta;
-  double x_t, y_t, x_0, y_0;
-  double t;
-  uint64_t seed;       // this step's sampler seed
-  int64_t step;
-  int32_t p, m, steps_for_slowing, episodes;
-  int32_t nv, nb;
+  EpisodeHead h;
   double grid_v[kEpMaxGrid];
   double grid_b[kEpMaxGrid];
+  uint32_t done;       // blocks of the running fused launch that have finished
+  uint32_t pad_;
 };
 
-__device__ inline Consts episode_consts(const EpisodeState& S, double x, double y, double phi,
+__device__ inline Consts episode_consts(const EpisodeHead& S, double x, double y, double phi,
                                         double L, double t_a, double t_b) {
   mpc_problem_t p;
   p.x = x;
@@ -54,7 +49,7 @@ __device__ inline Consts episode_consts(const EpisodeState& S, double x, double 
 // Episode.reset() / math_mpc's prologue (:521-541): start pose, target, line
 // origin at the start, t = 0, p = 1, m = 0, incumbent = control_criterion of
 // the line origin (the reference's first optimal_criterion, :676).
-__device__ inline void episode_restart(const mpc_episode_config_t& c, EpisodeState& S) {
+__device__ inline void episode_restart(const mpc_episode_config_t& c, EpisodeHead& S) {
   S.x = c.start_x;
   S.y = c.start_y;
   S.phi = c.start_phi;
@@ -73,17 +68,34 @@ __device__ inline void episode_restart(const mpc_episode_config_t& c, EpisodeSta
   S.incumbent = cost(S.x_0, S.y_0, K0);
 }
 
+__device__ __forceinline__ uint64_t episode_seed(const mpc_episode_config_t& c,
+                                                 const EpisodeHead& S) {
+  return c.seed + 0x9E3779B9ull * static_cast<uint64_t>(S.p + 1000 * S.episodes);
+}
+
+// Start of an MPC step (math_mpc :302): t += dt, this step's problem
+// constants (quad window [t, t+dt]) and sampler seed.  Run by reset and at
+// the end of every advance, so a step's rollout needs no preparation launch.
+__device__ inline void episode_prepare(const mpc_episode_config_t& c, EpisodeHead& S) {
+  const double t = S.t + c.delta_t;
+  S.K = episode_consts(S, S.x, S.y, S.phi, c.L, t, t + c.delta_t);
+  S.t = t;
+  S.seed = episode_seed(c, S);
+}
+
 __global__ void k_episode_reset(mpc_episode_config_t c, EpisodeState* __restrict__ S) {
   if (threadIdx.x != 0) return;
-  S->step = 0;
-  S->episodes = 0;
-  episode_restart(c, *S);
+  EpisodeHead H = {};
+  episode_restart(c, H);
+  episode_prepare(c, H);
+  S->h = H;
+  S->done = 0u;
 }
 
 // Grids (:239-256) with the reference's expressions and the slow-down
 // override (:312-316), computed by one wave: lane i evaluates grid point i,
 // a ballot compacts the accepted points in order.  Writes s_v[nv], s_b[nb].
-__device__ inline void episode_grids(const mpc_episode_config_t& c, const EpisodeState& S,
+__device__ inline void episode_grids(const mpc_episode_config_t& c, const EpisodeHead& S,
                                      double* s_v, double* s_b, int& nv_out, int& nb_out) {
   const int lane = threadIdx.x & 63;
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -122,11 +134,6 @@ __device__ inline void episode_grids(const mpc_episode_config_t& c, const Episod
   nb_out = nb < kEpMaxGrid ? nb : kEpMaxGrid;
 }
 
-__device__ __forceinline__ uint64_t episode_seed(const mpc_episode_config_t& c,
-                                                 const EpisodeState& S) {
-  return c.seed + 0x9E3779B9ull * static_cast<uint64_t>(S.p + 1000 * S.episodes);
-}
-
 __global__ __launch_bounds__(kBlock) void k_episode_sample(
     mpc_episode_config_t c, EpisodeState* __restrict__ S, int64_t n_cand, int n_steps,
     int64_t base, double* __restrict__ v, double* __restrict__ b, int pairs) {
@@ -135,7 +142,7 @@ __global__ __launch_bounds__(kBlock) void k_episode_sample(
   __shared__ int s_nv, s_nb;
   if (threadIdx.x < 64) {
     int nv, nb;
-    episode_grids(c, *S, s_v, s_b, nv, nb);
+    episode_grids(c, S->h, s_v, s_b, nv, nb);
     if (threadIdx.x == 0) {
       s_nv = nv;
       s_nb = nb;
@@ -143,18 +150,14 @@ __global__ __launch_bounds__(kBlock) void k_episode_sample(
   }
   __syncthreads();
   const int nv = s_nv, nb = s_nb;
-  const uint64_t seed = episode_seed(c, *S);
+  const uint64_t seed = S->h.seed;
   const uint32_t n_grid = static_cast<uint32_t>(nv) * static_cast<uint32_t>(nb);
   for (uint32_t k = threadIdx.x; k < n_grid; k += kBlock)  // nv, nb <= 64: fits in LDS
     s_grid[k] = make_double2(s_v[k / nb], s_b[k % nb]);
   __syncthreads();
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    const double t = S->t + c.delta_t;  // :302
-    S->K = episode_consts(*S, S->x, S->y, S->phi, c.L, t, t + c.delta_t);
-    S->t = t;
-    S->seed = seed;
-    S->nv = nv;
-    S->nb = nb;
+    S->h.nv = nv;
+    S->h.nb = nb;
     for (int i = 0; i < nv; ++i) S->grid_v[i] = s_v[i];
     for (int i = 0; i < nb; ++i) S->grid_b[i] = s_b[i];
   }
@@ -189,9 +192,12 @@ __device__ inline void turn_target(double ax, double ay, double aphi, double d, 
 }
 
 // Episode._advance: finishing logic (:392-414), events (:564-569), restart.
-__device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeState* __restrict__ S,
-                                       const mpc_result_t& r, mpc_episode_log_t* __restrict__ log,
+// Operates on a register copy of the episode scalars (the caller loads it
+// once and stores it back once).
+__device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeHead& H,
+                                       const Winner& r, mpc_episode_log_t* __restrict__ log,
                                        int cap) {
+  EpisodeHead* S = &H;
   S->steps_for_slowing -= 1;
   S->incumbent = 9223372036854775808.0;  // float(sys.maxsize), :428
   mpc_episode_log_t* L = (log && cap > 0) ? &log[S->step % cap] : nullptr;
@@ -213,13 +219,13 @@ __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeSta
       k = 1;
       S->m += 1;
     } else {
-      const double ex = S->x_t - r.traj[probe][0], ey = S->y_t - r.traj[probe][1];
+      const double ex = S->x_t - r.tr[probe][0], ey = S->y_t - r.tr[probe][1];
       if (ex * ex + ey * ey <= c.eps) S->m += 1;
     }
     k = k < last ? k : last;
-    S->x = r.traj[k][0];
-    S->y = r.traj[k][1];
-    S->phi = r.traj[k][2];
+    S->x = r.tr[k][0];
+    S->y = r.tr[k][1];
+    S->phi = r.tr[k][2];
     S->v = r.v;
     S->beta = r.beta;
     double tx, ty;
@@ -250,6 +256,7 @@ __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeSta
     const double ex = S->x_t - S->x, ey = S->y_t - S->y;
     if (ex * ex + ey * ey <= c.eps || S->p > c.max_steps) episode_restart(c, *S);
   }
+  episode_prepare(c, *S);
   if (L) {
     L->x = S->x;
     L->y = S->y;
@@ -260,8 +267,8 @@ __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeSta
 }
 
 __device__ void episode_hook(const mpc_episode_config_t& c, const EpisodeHook& h,
-                             const mpc_result_t& r) {
-  episode_advance(c, h.S, r, h.log, h.cap);
+                             const Winner& r, EpisodeHead& H) {
+  episode_advance(c, H, r, h.log, h.cap);
 }
 
 // Multi-GPU: lexicographic (cost, global index) selection over the gathered
@@ -270,11 +277,21 @@ __global__ void k_episode_advance(mpc_episode_config_t c, EpisodeState* __restri
                                   const mpc_result_t* __restrict__ res, int n,
                                   mpc_episode_log_t* __restrict__ log, int cap) {
   if (threadIdx.x != 0) return;
+  EpisodeHead H = S->h;
   uint64_t bk;
   const int best = select_index(res, n, bk);
-  mpc_result_t w = res[best];
-  w.found = (bk != ~0ull && w.cost < S->incumbent) ? 1 : 0;
-  episode_advance(c, S, w, log, cap);
+  const mpc_result_t& r = res[best];
+  Winner w;
+  w.cost = r.cost;
+  w.index = r.index;
+  w.found = (bk != ~0ull && r.cost < H.incumbent) ? 1 : 0;
+  w.n_steps = r.n_steps;
+  w.v = r.v;
+  w.beta = r.beta;
+  for (int k = 0; k < 3; ++k)
+    for (int q = 0; q < 3; ++q) w.tr[k][q] = r.traj[k < r.n_steps ? k : 0][q];
+  episode_advance(c, H, w, log, cap);
+  S->h = H;
 }
 
 }  // namespace mpc

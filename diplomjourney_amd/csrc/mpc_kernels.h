@@ -207,21 +207,46 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
       reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p));
 }
 
-// Both control rows of one step into LDS (v at dst_v, beta at dst_v + 1 KiB).
-__device__ __forceinline__ void glds_step(const double* gv, const double* gb, uint32_t dst_v) {
+// Both control rows of one step into LDS (v at dst_v, beta at dst_b).  The
+// statement writes only M0 (saved and restored) and `keep`: no SCC-setting
+// instruction (s_add etc.), since hipcc may hold a live SCC across it.
+// Refilling a slot must not overtake the LDS reads of its previous contents:
+// `read_v`/`read_b` are the registers those reads produced, taken as inputs
+// so hipcc completes the reads (lgkmcnt) before the DMA is issued — without a
+// blanket lgkmcnt(0), which would also wait for unrelated scalar loads.
+__device__ __forceinline__ void glds_pair(const double* gv, const double* gb, uint32_t dst_v,
+                                          uint32_t dst_b) {
   uint32_t keep;
   asm volatile(
-      "s_waitcnt lgkmcnt(0)\n\t"
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %3\n\t"
       "s_nop 0\n\t"
       "global_load_lds_dwordx4 %1, off\n\t"
-      "s_add_u32 m0, %3, 0x400\n\t"
+      "s_mov_b32 m0, %4\n\t"
       "s_nop 0\n\t"
       "global_load_lds_dwordx4 %2, off\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(gv), "v"(gb), "s"(dst_v)
+      : "v"(gv), "v"(gb), "s"(dst_v), "s"(dst_b)
+      : "memory");
+}
+
+__device__ __forceinline__ void glds_refill(const double* gv, const double* gb, uint32_t dst_v,
+                                            uint32_t dst_b, const double2& read_v,
+                                            const double2& read_b) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %4\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gv), "v"(gb), "s"(dst_v), "s"(dst_b), "v"(read_v.x), "v"(read_v.y),
+        "v"(read_b.x), "v"(read_b.y)
       : "memory");
 }
 
@@ -256,9 +281,7 @@ __device__ __forceinline__ void rollout_lane_glds(const Consts& K, const double*
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ring0 = __builtin_amdgcn_readfirstlane(lds_addr(&g_ring[wv][0][0][0]));
   constexpr uint32_t kSlot = 2 * 64 * sizeof(double2);  // 2 KiB
-  auto issue = [&](int sr, int slot) {
-    glds_step(v + sr * ld + c0, b + sr * ld + c0, ring0 + slot * kSlot);
-  };
+  auto dst = [&](int slot) { return ring0 + slot * kSlot; };
   double x[CPL], y[CPL], ph[CPL], sn[CPL], cs[CPL];
   bool bad[CPL];
 #pragma unroll
@@ -272,7 +295,9 @@ __device__ __forceinline__ void rollout_lane_glds(const Consts& K, const double*
   }
 #pragma unroll
   for (int u = 0; u < R - 1; ++u)
-    if (u < n_steps) issue(u, u);
+    if (u < n_steps)
+      glds_pair(v + u * ld + c0, b + u * ld + c0, dst(u), dst(u) + kSlot / 2);
+  double2 v2 = make_double2(0.0, 0.0), b2 = v2;   // the last slot's contents as read
 #pragma unroll 1
   for (int s = 0; s < n_steps; s += R) {
 #pragma unroll
@@ -280,13 +305,15 @@ __device__ __forceinline__ void rollout_lane_glds(const Consts& K, const double*
       const int st = s + u;
       if (st < n_steps) {
         if (st + R - 1 < n_steps) {
-          issue(st + R - 1, (u + R - 1) % R);
+          const int sr = st + R - 1, slot = (u + R - 1) % R;   // = the slot read last step
+          glds_refill(v + sr * ld + c0, b + sr * ld + c0, dst(slot), dst(slot) + kSlot / 2, v2,
+                      b2);
           wait_vm<2 * (R - 1)>();   // this step's pair has landed
         } else {
           wait_vm<0>();             // pipeline tail
         }
-        const double2 v2 = g_ring[wv][u][0][lane];
-        const double2 b2 = g_ring[wv][u][1][lane];
+        v2 = g_ring[wv][u][0][lane];
+        b2 = g_ring[wv][u][1][lane];
         step_core<INTEG, ROT, PL2>(x[0], y[0], ph[0], sn[0], cs[0], v2.x, b2.x, K, bad[0]);
         step_core<INTEG, ROT, PL2>(x[1], y[1], ph[1], sn[1], cs[1], v2.y, b2.y, K, bad[1]);
       }
@@ -354,6 +381,16 @@ __global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(
   if (threadIdx.x == 0) part[blockIdx.x] = Rec{best_k, best_i};
 }
 
+// What the episode update needs of a winner (kept in registers by the
+// finalize kernel instead of being re-read from the result record).
+struct Winner {
+  double cost;
+  int64_t index;
+  int32_t found, n_steps;
+  double v, beta;
+  double tr[3][3];     // states of steps 0..2 (clamped to the horizon)
+};
+
 // Re-roll the winner and fill the result record.  Called by ALL threads of
 // the block once thread 0 holds the winner (key, col).  The N-step recurrence
 // is split so that only cheap accumulations stay serial: lane s computes the
@@ -367,7 +404,7 @@ template <int INTEG, bool ROT>
 __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
                             const double* __restrict__ b, int64_t ld, int n_steps, uint64_t key,
                             int64_t col, int64_t reported_index, double incumbent,
-                            mpc_result_t* __restrict__ out) {
+                            mpc_result_t* __restrict__ out, Winner* win = nullptr) {
   __shared__ double s_v[MPC_MAX_STEPS], s_dphi[MPC_MAX_STEPS], s_phi[MPC_MAX_STEPS];
   __shared__ double s_a[MPC_MAX_STEPS], s_c[MPC_MAX_STEPS];
   __shared__ double s_b0;
@@ -431,20 +468,34 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
   __syncthreads();
   if (lane != 0) return;
   out->n_steps = n_steps;
+  if (win) win->n_steps = n_steps;
   if (!valid) {
     out->cost = __builtin_inf();
     out->index = -1;
     out->found = 0;
     out->v = 0.0;
     out->beta = 0.0;
+    if (win) {
+      win->cost = __builtin_inf();
+      win->index = -1;
+      win->found = 0;
+    }
     return;
   }
   const double c = key_cost(key);
+  const int found = c < incumbent ? 1 : 0;
   out->cost = c;
   out->index = s_rep;
-  out->found = c < incumbent ? 1 : 0;
+  out->found = found;
   out->v = s_v[0];
   out->beta = s_b0;
+  if (win) {
+    win->cost = c;
+    win->index = s_rep;
+    win->found = found;
+    win->v = s_v[0];
+    win->beta = s_b0;
+  }
   double x = K.x, y = K.y, sn = K.s0, cs = K.c0;
   for (int st = 0; st < n_steps; ++st) {
     if (ROT && !bad) {
@@ -458,17 +509,124 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
     out->traj[st][0] = x;
     out->traj[st][1] = y;
     out->traj[st][2] = s_phi[st];
+    if (win && st < 3) {
+      win->tr[st][0] = x;
+      win->tr[st][1] = y;
+      win->tr[st][2] = s_phi[st];
+    }
   }
 }
 
-struct EpisodeState;
+// The device-resident episode's scalars (mpc_episode.h: EpisodeState = this
+// head + the sampler grids).
+struct EpisodeHead {
+  Consts K;            // this step's problem constants
+  double incumbent;    // optimal_criterion at the start of this step
+  double x, y, phi, v, beta;
+  double x_t, y_t, x_0, y_0;
+  double t;
+  uint64_t seed;       // this step's sampler seed
+  int64_t step;
+  int32_t p, m, steps_for_slowing, episodes;
+  int32_t nv, nb;
+};
+
 struct EpisodeHook {  // single-GPU episode: finalize also advances it
-  EpisodeState* S;    // nullptr: no hook
+  EpisodeHead* H;     // nullptr: no hook
   mpc_episode_log_t* log;
   int cap;
 };
 __device__ void episode_hook(const mpc_episode_config_t& c, const EpisodeHook& h,
-                             const mpc_result_t& r);
+                             const Winner& r, EpisodeHead& H);
+
+// Block-record reduction + winner re-roll (+ episode update), run by every
+// thread of one block of NT threads.  SC1: the records were written by
+// blocks of the SAME launch (fused path): they were stored `sc1` and are read
+// `sc1` (L1 bypassed; the counter hand-off of rollout_episode).
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+// Eight records, `sc1`, in ONE statement that also waits for them: an asm
+// load's destination is written whenever the data arrives, so it must never
+// leave the statement un-waited (hipcc may copy or reuse the register).
+__device__ __forceinline__ void load8_rec_sc1(const Rec* const (&p)[8], u64x2 (&r)[8]) {
+  asm volatile(
+      "global_load_dwordx4 %0, %8, off sc1\n\t"
+      "global_load_dwordx4 %1, %9, off sc1\n\t"
+      "global_load_dwordx4 %2, %10, off sc1\n\t"
+      "global_load_dwordx4 %3, %11, off sc1\n\t"
+      "global_load_dwordx4 %4, %12, off sc1\n\t"
+      "global_load_dwordx4 %5, %13, off sc1\n\t"
+      "global_load_dwordx4 %6, %14, off sc1\n\t"
+      "global_load_dwordx4 %7, %15, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]),
+        "=&v"(r[6]), "=&v"(r[7])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
+      : "memory");
+}
+
+template <int INTEG, bool ROT, bool KDEV, int NT, bool SC1>
+__device__ __forceinline__ void finalize_block(
+    const Rec* __restrict__ part, int n_part, const Consts& K, const double* __restrict__ v,
+    const double* __restrict__ b, int64_t n_cand, int n_steps, int64_t index_base,
+    double incumbent, mpc_result_t* __restrict__ out, const mpc_episode_config_t& ecfg,
+    const EpisodeHook& hook) {
+  // One-GPU episode: thread 0 loads the episode scalars now, in parallel with
+  // everything below, and stores them back once after the update.
+  EpisodeHead H;
+  if (KDEV && hook.H && threadIdx.x == 0) H = *hook.H;
+  __shared__ uint64_t s_key[NT / 64];
+  __shared__ int64_t s_idx[NT / 64];
+  uint64_t k = ~0ull;
+  int64_t i = INT64_MAX;
+  if constexpr (SC1) {
+    // n_part <= kMaxBlocks = 8 * NT: eight loads per thread, addresses of
+    // out-of-range slots clamped to a valid record and their values ignored
+    static_assert(kMaxBlocks <= 8 * NT, "load8_rec_sc1 covers 8 records per thread");
+    const Rec* ptr[8];
+    u64x2 r[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int p = threadIdx.x + q * NT;
+      ptr[q] = part + (p < n_part ? p : n_part - 1);
+    }
+    load8_rec_sc1(ptr, r);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (threadIdx.x + q * NT < n_part &&
+          rec_less(r[q].x, static_cast<int64_t>(r[q].y), k, i)) {
+        k = r[q].x;
+        i = static_cast<int64_t>(r[q].y);
+      }
+  } else {
+    for (int p = threadIdx.x; p < n_part; p += NT) {
+      const Rec r = part[p];
+      if (rec_less(r.key, r.idx, k, i)) {
+        k = r.key;
+        i = r.idx;
+      }
+    }
+  }
+  wave_argmin(k, i);
+  if ((threadIdx.x & 63) == 0) {
+    s_key[threadIdx.x >> 6] = k;
+    s_idx[threadIdx.x >> 6] = i;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < NT / 64; ++w)
+      if (rec_less(s_key[w], s_idx[w], k, i)) {
+        k = s_key[w];
+        i = s_idx[w];
+      }
+  }
+  Winner w;
+  emit_winner<INTEG, ROT>(K, v, b, n_cand, n_steps, k, i, index_base + i, incumbent, out, &w);
+  if (KDEV && hook.H && threadIdx.x == 0) {
+    episode_hook(ecfg, hook, w, H);
+    *hook.H = H;
+  }
+}
 
 template <int INTEG, bool ROT, bool KDEV>
 __global__ __launch_bounds__(kFinBlock) void k_finalize(
@@ -478,30 +636,61 @@ __global__ __launch_bounds__(kFinBlock) void k_finalize(
     mpc_result_t* __restrict__ out, mpc_episode_config_t ecfg, EpisodeHook hook) {
   const Consts K = KDEV ? *Kdev : Karg;
   const double incumbent = KDEV ? *incumbent_dev : incumbent_arg;
-  __shared__ uint64_t s_key[kFinBlock / 64];
-  __shared__ int64_t s_idx[kFinBlock / 64];
-  uint64_t k = ~0ull;
-  int64_t i = INT64_MAX;
-  for (int p = threadIdx.x; p < n_part; p += kFinBlock)
-    if (rec_less(part[p].key, part[p].idx, k, i)) {
-      k = part[p].key;
-      i = part[p].idx;
+  finalize_block<INTEG, ROT, KDEV, kFinBlock, false>(part, n_part, K, v, b, n_cand, n_steps,
+                                                     index_base, incumbent, out, ecfg, hook);
+}
+
+// Device-resident episode, one launch per MPC step: the streaming rollout +
+// block arg-min of k_rollout_argmin, then the LAST block to finish runs the
+// finalize (record reduction, winner re-roll, and on one GPU the episode
+// update).  Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): each
+// block's thread 0 stores its record `sc1`, waits for it (vmcnt(0)), then adds
+// to the launch counter (agent-scope atomic); the block whose add returns
+// gridDim-1 is last, and its threads read every record `sc1` after a
+// workgroup barrier.  The last block re-arms the counter for the next launch.
+template <int CPL, int INTEG, bool ROT>
+__global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_episode(
+    const Consts* __restrict__ Kdev, const double* __restrict__ v, const double* __restrict__ b,
+    int64_t n_cand, int n_steps, int64_t index_base, Rec* __restrict__ part,
+    uint32_t* __restrict__ done, const double* __restrict__ incumbent_dev,
+    mpc_result_t* __restrict__ out, mpc_episode_config_t ecfg, EpisodeHook hook) {
+  const Consts K = *Kdev;
+  const int64_t n_tiles = (n_cand + kBlock * CPL - 1) / (kBlock * CPL);
+  uint64_t best_k = ~0ull;
+  int64_t best_i = INT64_MAX;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int64_t c0 = tile * (kBlock * CPL) + threadIdx.x * CPL;
+    if (c0 < n_cand) {
+      double cst[CPL];
+      rollout_lane<CPL, INTEG, ROT, false>(K, v, b, n_cand, c0, n_steps, cst, nullptr, n_cand);
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        const uint64_t kk = cost_key(cst[j]);
+        if (kk < best_k) {
+          best_k = kk;
+          best_i = c0 + j;
+        }
+      }
     }
-  wave_argmin(k, i);
-  if ((threadIdx.x & 63) == 0) {
-    s_key[threadIdx.x >> 6] = k;
-    s_idx[threadIdx.x >> 6] = i;
+  }
+  block_argmin(best_k, best_i);
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+    Rec* dst = part + blockIdx.x;
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)"
+                 :
+                 : "v"(dst),
+                   "v"(u64x2{best_k, static_cast<uint64_t>(best_i)})
+                 : "memory");
+    const uint32_t prev =
+        __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == gridDim.x - 1;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < kFinBlock / 64; ++w)
-      if (rec_less(s_key[w], s_idx[w], k, i)) {
-        k = s_key[w];
-        i = s_idx[w];
-      }
-  }
-  emit_winner<INTEG, ROT>(K, v, b, n_cand, n_steps, k, i, index_base + i, incumbent, out);
-  if (KDEV && hook.S && threadIdx.x == 0) episode_hook(ecfg, hook, *out);
+  if (!s_last) return;
+  finalize_block<INTEG, ROT, true, kBlock, true>(part, gridDim.x, K, v, b, n_cand, n_steps,
+                                                 index_base, *incumbent_dev, out, ecfg, hook);
+  if (threadIdx.x == 0) *done = 0u;
 }
 
 // Problem constants derived on the device (batched robots, episode).  The

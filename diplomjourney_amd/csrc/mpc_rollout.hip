@@ -100,6 +100,30 @@ void dispatch_mode(int32_t integrator, F&& f) {
   }
 }
 
+// Resident blocks of one fused episode instantiation (occupancy x CUs), cached
+// per instantiation and device.  The fused launch is sized to ONE resident
+// round: each block's end-of-launch hand-off (sc1 store + counter atomic) is
+// then paid once per block, not once per tile round.
+template <int CPL, int I, bool R>
+int64_t fused_grid(int64_t n_cand) {
+  static int64_t cache[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+  if (cache[dev] == 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, reinterpret_cast<const void*>(&k_rollout_episode<CPL, I, R>), kBlock, 0) !=
+            hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus < 1)
+      cus = 256;
+    cache[dev] = std::min<int64_t>(static_cast<int64_t>(per_cu) * cus, kMaxBlocks);
+  }
+  return std::max<int64_t>(1, std::min(cdiv(n_cand, kBlock * CPL), cache[dev]));
+}
+
 // Number of block records the rollout launch for these arguments writes
 // (= its grid); the finalize launch reduces exactly these.
 int64_t partial_count(const double* v_sc, const double* beta_sc, int64_t n_cand,
@@ -344,7 +368,7 @@ int mpc_episode_partials(void* state, const double* v_sc, const double* beta_sc,
   if (mode_ok(integrator) != MPC_OK) return MPC_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
   EpisodeState* S = static_cast<EpisodeState*>(state);
-  launch_rollout<true>(reinterpret_cast<hipStream_t>(stream), integrator, Consts{}, &S->K, v_sc,
+  launch_rollout<true>(reinterpret_cast<hipStream_t>(stream), integrator, Consts{}, &S->h.K, v_sc,
                        beta_sc, n_cand, n_steps, static_cast<Rec*>(ws));
   return last_hip_status();
 }
@@ -362,10 +386,40 @@ int mpc_episode_finalize(void* state, const double* v_sc, const double* beta_sc,
   EpisodeState* S = static_cast<EpisodeState*>(state);
   const int n_part = static_cast<int>(partial_count(v_sc, beta_sc, n_cand, false));
   const mpc_episode_config_t ecfg = advance ? *advance : mpc_episode_config_t{};
-  const EpisodeHook hook{advance ? S : nullptr, log, log_capacity};
+  const EpisodeHook hook{advance ? &S->h : nullptr, log, log_capacity};
   launch_finalize<true>(reinterpret_cast<hipStream_t>(stream), integrator,
-                        static_cast<const Rec*>(ws), n_part, Consts{}, &S->K, v_sc, beta_sc,
-                        n_cand, n_steps, index_base, 0.0, &S->incumbent, out, ecfg, hook);
+                        static_cast<const Rec*>(ws), n_part, Consts{}, &S->h.K, v_sc, beta_sc,
+                        n_cand, n_steps, index_base, 0.0, &S->h.incumbent, out, ecfg, hook);
+  return last_hip_status();
+}
+
+int mpc_episode_rollout(void* state, const double* v_sc, const double* beta_sc, int64_t n_cand,
+                        int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
+                        size_t ws_bytes, mpc_result_t* out, const mpc_episode_config_t* advance,
+                        mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream) {
+  if (check_episode_arrays(state, v_sc, beta_sc, n_cand, n_steps) != MPC_OK || !out ||
+      index_base < 0)
+    return MPC_ERR_ARG;
+  if (mode_ok(integrator) != MPC_OK) return MPC_ERR_UNSUPPORTED;
+  if (!ws || ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
+  if (advance && (check_episode_cfg(advance) != MPC_OK || log_capacity < 0)) return MPC_ERR_ARG;
+  EpisodeState* S = static_cast<EpisodeState*>(state);
+  const mpc_episode_config_t ecfg = advance ? *advance : mpc_episode_config_t{};
+  const EpisodeHook hook{advance ? &S->h : nullptr, log, log_capacity};
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const bool wide = wide_ok(v_sc, beta_sc, n_cand);
+  dispatch_mode(integrator, [&](auto integ, auto rot) {
+    constexpr int I = decltype(integ)::value;
+    constexpr bool R = decltype(rot)::value;
+    if (wide)
+      k_rollout_episode<kCplWide, I, R><<<fused_grid<kCplWide, I, R>(n_cand), kBlock, 0, st>>>(
+          &S->h.K, v_sc, beta_sc, n_cand, n_steps, index_base, static_cast<Rec*>(ws), &S->done,
+          &S->h.incumbent, out, ecfg, hook);
+    else
+      k_rollout_episode<1, I, R><<<fused_grid<1, I, R>(n_cand), kBlock, 0, st>>>(
+          &S->h.K, v_sc, beta_sc, n_cand, n_steps, index_base, static_cast<Rec*>(ws), &S->done,
+          &S->h.incumbent, out, ecfg, hook);
+  });
   return last_hip_status();
 }
 
@@ -374,13 +428,11 @@ int mpc_episode_expand(const mpc_episode_config_t* cfg, void* state, double* v_s
                        int32_t integrator, void* ws, size_t ws_bytes, mpc_result_t* out,
                        mpc_stream_t stream) {
   if (!out) return MPC_ERR_ARG;
-  int a = mpc_episode_sample(cfg, state, v_sc, beta_sc, n_cand, n_steps, index_base, stream);
+  const int a =
+      mpc_episode_sample(cfg, state, v_sc, beta_sc, n_cand, n_steps, index_base, stream);
   if (a != MPC_OK) return a;
-  a = mpc_episode_partials(state, v_sc, beta_sc, n_cand, n_steps, integrator, ws, ws_bytes,
-                           stream);
-  if (a != MPC_OK) return a;
-  return mpc_episode_finalize(state, v_sc, beta_sc, n_cand, n_steps, index_base, integrator, ws,
-                              ws_bytes, out, nullptr, nullptr, 0, stream);
+  return mpc_episode_rollout(state, v_sc, beta_sc, n_cand, n_steps, index_base, integrator, ws,
+                             ws_bytes, out, nullptr, nullptr, 0, stream);
 }
 
 int mpc_episode_advance(const mpc_episode_config_t* cfg, void* state, const mpc_result_t* results,

@@ -178,7 +178,7 @@ class DeviceEpisode:
 
     def __init__(self, engine, n_cand_total, n_steps, rank=0, world=1, seed=20261015,
                  integrator="rect", group=None, start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3),
-                 log_capacity=4096):
+                 log_capacity=4096, split=True):
         self.eng = engine
         self.lib = native.lib()
         self.n_total = int(n_cand_total)
@@ -201,6 +201,8 @@ class DeviceEpisode:
                               dtype=torch.uint8, device=dev)
         from .abi import INTEGRATORS
         self._integ = INTEGRATORS[integrator]
+        self.cur = (self.v_sc, self.b_sc)
+        self.split = bool(split)
         self.steps_enqueued = 0
         self.reset()
 
@@ -212,35 +214,59 @@ class DeviceEpisode:
                                                 self._stream()), "mpc_episode_reset")
         self.steps_enqueued = 0
 
-    def expand(self, events=None):
+    def expand(self, events=None, controls=None):
         """Grid + sampler + rollout + finalize for this rank's shard.
+        controls: optional caller-resident (v_sc, beta_sc) fp64 [n_steps,
+        n_local] for this step — the rollout streams them instead of the
+        sampler's (the candidate set is the caller's input).
         events: optional (start, stop) torch.cuda.Event pair recorded around
-        the streaming rollout kernel alone."""
+        the rollout (+ selection) launch."""
         st = self._stream()
         L = self.lib
-        native.check(L.mpc_episode_sample(ctypes.byref(self.cfg), self.state.data_ptr(),
-                                          self.v_sc.data_ptr(), self.b_sc.data_ptr(),
-                                          self.n_local, self.n_steps, self.lo, st),
-                     "mpc_episode_sample")
+        if controls is None:
+            native.check(L.mpc_episode_sample(ctypes.byref(self.cfg), self.state.data_ptr(),
+                                              self.v_sc.data_ptr(), self.b_sc.data_ptr(),
+                                              self.n_local, self.n_steps, self.lo, st),
+                         "mpc_episode_sample")
+            self.cur = (self.v_sc, self.b_sc)
+        else:
+            v, b = controls
+            if (tuple(v.shape) != (self.n_steps, self.n_local) or v.shape != b.shape
+                    or v.dtype != torch.float64 or b.dtype != torch.float64
+                    or not v.is_contiguous() or not b.is_contiguous()
+                    or v.device != self.v_sc.device or b.device != self.v_sc.device):
+                raise ValueError("controls must be contiguous float64 [n_steps, n_local] "
+                                 "tensors on the episode's device")
+            self.cur = (v, b)
+        one_gpu = self.world == 1    # one GPU: the step's launch also advances the episode
+        args = (self.state.data_ptr(), self.cur[0].data_ptr(), self.cur[1].data_ptr(),
+                self.n_local, self.n_steps, self.lo, self._integ, self.ws.data_ptr(),
+                self.ws.numel(), self.local.data_ptr(),
+                ctypes.byref(self.cfg) if one_gpu else None,
+                self.log.data_ptr() if one_gpu else None, self.log_capacity if one_gpu else 0, st)
         if events:
             events[0].record()
-        native.check(L.mpc_episode_partials(self.state.data_ptr(), self.v_sc.data_ptr(),
-                                            self.b_sc.data_ptr(), self.n_local, self.n_steps,
-                                            self._integ, self.ws.data_ptr(), self.ws.numel(), st),
-                     "mpc_episode_partials")
+        if self.split:
+            # streaming kernel, then the selection kernel (two launches; the
+            # faster form on MI355X: 44.8 vs 47.5 us per config-C step)
+            self.partials(st)
+            native.check(L.mpc_episode_finalize(*args), "mpc_episode_finalize")
+        else:
+            # one launch: the last block to finish runs the selection
+            native.check(L.mpc_episode_rollout(*args), "mpc_episode_rollout")
         if events:
             events[1].record()
-        fused = self.world == 1    # one GPU: finalize also advances the episode
-        native.check(L.mpc_episode_finalize(self.state.data_ptr(), self.v_sc.data_ptr(),
-                                            self.b_sc.data_ptr(), self.n_local, self.n_steps,
-                                            self.lo, self._integ, self.ws.data_ptr(),
-                                            self.ws.numel(), self.local.data_ptr(),
-                                            ctypes.byref(self.cfg) if fused else None,
-                                            self.log.data_ptr() if fused else None,
-                                            self.log_capacity if fused else 0, st),
-                     "mpc_episode_finalize")
-        if fused:
+        if one_gpu:
             self.steps_enqueued += 1
+
+    def partials(self, st=None):
+        """The streaming rollout/arg-min kernel alone on the current controls
+        (writes only the workspace block records; the episode is unchanged)."""
+        v, b = self.cur
+        native.check(self.lib.mpc_episode_partials(
+            self.state.data_ptr(), v.data_ptr(), b.data_ptr(), self.n_local,
+            self.n_steps, self._integ, self.ws.data_ptr(), self.ws.numel(),
+            st if st is not None else self._stream()), "mpc_episode_partials")
 
     def advance(self):
         """Multi-GPU: all_gather of the per-rank winners (RCCL) + selection +
@@ -254,8 +280,8 @@ class DeviceEpisode:
             self.log.data_ptr(), self.log_capacity, self._stream()), "mpc_episode_advance")
         self.steps_enqueued += 1
 
-    def step(self, events=None):
-        self.expand(events)
+    def step(self, events=None, controls=None):
+        self.expand(events, controls)
         self.advance()
 
     def read_log(self):

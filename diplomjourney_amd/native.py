@@ -30,7 +30,7 @@ EXPORTS = (
     "mpc_batched_workspace_bytes", "mpc_rollout_argmin_batched", "mpc_select_winner",
     "mpc_sample_controls", "mpc_episode_state_bytes", "mpc_episode_reset",
     "mpc_episode_expand", "mpc_episode_advance", "mpc_episode_sample", "mpc_episode_partials",
-    "mpc_episode_finalize",
+    "mpc_episode_finalize", "mpc_episode_rollout",
 )
 
 HIPCC_FLAGS = [
@@ -121,6 +121,9 @@ def lib():
     L.mpc_episode_finalize.restype = ctypes.c_int
     L.mpc_episode_finalize.argtypes = [_P, _P, _P, _I64, _I32, _I64, _I32, _P, ctypes.c_size_t,
                                        _P, ctypes.POINTER(MpcEpisodeConfig), _P, _I32, _P]
+    L.mpc_episode_rollout.restype = ctypes.c_int
+    L.mpc_episode_rollout.argtypes = [_P, _P, _P, _I64, _I32, _I64, _I32, _P, ctypes.c_size_t,
+                                      _P, ctypes.POINTER(MpcEpisodeConfig), _P, _I32, _P]
     _lib = L
     return L
 

@@ -146,14 +146,17 @@ int mpc_sample_controls(const double* v_grid, int32_t n_v, const double* beta_gr
  * Device-resident MPC episode: the reference's math_mpc loop
  * (math_model_tree.py:515-635) with its state in HBM, so an MPC step is
  * enqueued with no host synchronisation (graph-capturable):
- *   mpc_episode_expand   grid (:239-256, slow-down :312-316) + t += dt
- *                        (:302) + sampler + rollout + finalize -> local winner
+ *   mpc_episode_expand   grid (:239-256, slow-down :312-316) + sampler +
+ *                        rollout + finalize -> local winner
  *   mpc_episode_advance  [multi-GPU: over the all_gather'ed per-rank winners,
  *                        lexicographic (cost, index) selection first]
  *                        finishing logic (:392-414), operator events
- *                        (:564-569), arrival/step-limit restart, one log record
- * On one GPU, mpc_episode_finalize can apply the advance itself (`advance`
- * non-NULL), so a step is three launches.
+ *                        (:564-569), arrival/step-limit restart, one log
+ *                        record, then the next step's t += dt (:302), problem
+ *                        constants and sampler seed (also done by reset)
+ * On one GPU the fused mpc_episode_rollout applies the advance itself
+ * (`advance` non-NULL), so a step is two launches (sampler + rollout) — one
+ * when the caller supplies the step's candidate controls.
  * The grid ratios are passed precomputed with the reference's expressions.
  * ------------------------------------------------------------------------- */
 typedef struct mpc_episode_config {
@@ -188,8 +191,17 @@ int mpc_episode_expand(const mpc_episode_config_t* cfg, void* state, double* v_s
 int mpc_episode_advance(const mpc_episode_config_t* cfg, void* state, const mpc_result_t* results,
                         int32_t n_results, mpc_episode_log_t* log, int32_t log_capacity,
                         mpc_stream_t stream);
-/* The three launches of mpc_episode_expand, separately (timing, overlap):
- * grid + t + problem + sampler | streaming rollout kernel | selection. */
+/* One launch: streaming rollout + block arg-min, and the last block to finish
+ * reduces the block records, re-rolls the winner into `out` and (advance
+ * non-NULL, one GPU) applies the episode update.  The step's candidates are
+ * v_sc/beta_sc: the sampler's (mpc_episode_sample) or the caller's own.
+ * mpc_episode_expand = mpc_episode_sample + this. */
+int mpc_episode_rollout(void* state, const double* v_sc, const double* beta_sc, int64_t n_cand,
+                        int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
+                        size_t ws_bytes, mpc_result_t* out, const mpc_episode_config_t* advance,
+                        mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
+/* The launches separately (timing, overlap): grid + sampler | streaming
+ * rollout kernel | selection [+ advance]. */
 int mpc_episode_sample(const mpc_episode_config_t* cfg, void* state, double* v_sc,
                        double* beta_sc, int64_t n_cand, int32_t n_steps, int64_t index_base,
                        mpc_stream_t stream);

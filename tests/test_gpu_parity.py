@@ -280,11 +280,13 @@ def test_two_phase_api_matches(engine):
     assert bytes(one) == bytes(two)
 
 
-def test_device_episode_matches_host_episode(engine):
+@pytest.mark.parametrize("split", [False, True])
+def test_device_episode_matches_host_episode(engine, split):
     """The device-resident episode (mpc_episode_*: grid, sampler, problem,
     finishing logic and operator events in HBM, no host sync) makes the same
     choices as the host-driven episode over 200 MPC steps incl. the
-    p = 60 / 90 / 110 operator events."""
+    p = 60 / 90 / 110 operator events — with the selection run by the last
+    block of the rollout launch (fused) or by its own kernel (split)."""
     from diplomjourney_amd.episode import DeviceEpisode, Episode
     n, ns, steps = 20_000, 10, 200
     host = Episode(engine, n, ns)
@@ -294,7 +296,7 @@ def test_device_episode_matches_host_episode(engine):
         r = host.step()
         want.append((r.index if r.found else -1, r.cost, p, host.x, host.y, host.phi, host.v,
                      host.beta))
-    dev = DeviceEpisode(engine, n, ns, log_capacity=512)
+    dev = DeviceEpisode(engine, n, ns, log_capacity=512, split=split)
     for _ in range(steps):
         dev.step()
     got = dev.read_log()
@@ -304,3 +306,43 @@ def test_device_episode_matches_host_episode(engine):
         assert math.isclose(g.cost, w[1], rel_tol=COST_RTOL)
         assert max(abs(a - b) for a, b in zip((g.x, g.y, g.phi, g.v, g.beta), w[3:])) <= STATE_TOL
     assert max(w[2] for w in want) > 110          # the operator events were exercised
+
+
+@pytest.mark.parametrize("integ", ["rect+rot", "qk21", "rect", "qk21+rot"])
+def test_device_episode_resident_controls(engine, integ):
+    """Device episode over caller-resident candidate batches (the bench's
+    default input mode: no sampler launch, the step's problem prepared by the
+    previous advance).  Every step's winner equals the plain C-ABI arg-min of
+    the same batch on the problem rebuilt on the host from the previous
+    logged state, and the partial records of the device-constants (KDEV)
+    kernel equal those of the by-value kernel."""
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.abi import make_problem
+    from diplomjourney_amd.episode import DeviceEpisode
+    n, ns, steps = 50_000, 10, 6
+    dev = DeviceEpisode(engine, n, ns, integrator=integ, log_capacity=64)
+    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
+    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
+    pool = [engine.sample_controls(V, B, n, ns, 77 + i) for i in range(steps)]
+    x = y = phi = 0.0
+    t, dt = 0.0, mmt.delta_t
+    for i in range(steps):
+        t = t + dt
+        prob = make_problem(x, y, phi, 2, 3, 0, 0, mmt.L, t, t + dt)
+        inc = 10000 * math.sqrt(13) + 10000 * 1000 ** 2 if i == 0 else INC_MAX
+        dev.cur = pool[i]
+        dev.partials()                               # KDEV records of this batch ...
+        kdev = dev.ws.clone()
+        dev.step(controls=pool[i])
+        ref = engine.fetch(engine.rollout_argmin(prob, *pool[i], incumbent=inc,
+                                                 integrator=integ))
+        log = dev.read_log()[-1]
+        assert log.index == ref.index and ref.found == 1
+        assert math.isclose(log.cost, ref.cost, rel_tol=COST_RTOL)
+        engine.partials(prob, *pool[i], integ)       # ... equal the by-value kernel's
+        n_rec = -(-n // 512)                         # blocks of the CPL = 2 launch
+        a = kdev.view(torch.int64)[:2 * n_rec].cpu()
+        b = engine._workspace(engine.lib.mpc_workspace_bytes(n, ns)).view(torch.int64)[:2 * n_rec].cpu()
+        idx_a, idx_b = a[1::2], b[1::2]
+        assert torch.equal(idx_a, idx_b)
+        x, y, phi = log.x, log.y, log.phi
