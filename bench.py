@@ -89,8 +89,9 @@ def parse():
                     help="override the workload's per-GPU candidate count")
     ap.add_argument("--dump-log", default=None,
                     help="write the device episode's per-step log (rank 0) to this JSON file")
-    ap.add_argument("--traffic-json", default=None,
-                    help="PMC-derived HBM bytes per launch for the roofline 'traffic' field")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r01_traffic.json"),
+                    help="PMC-derived HBM bytes per launch for the roofline 'traffic' field "
+                         "(tools/pmc.sh + tools/pmc_summary.py on the same kernel and config)")
     return ap.parse_args()
 
 
@@ -156,7 +157,8 @@ def main():
     main_run = run_steps(args, ep, pool, use_graph, world, device)
     kern_ms = main_run["kernel_in_step_ms"]
     if hasattr(ep, "partials"):
-        kern_ms = kernel_pass(ep)
+        kern_ms = kernel_pass(ep, pool if pool is not None else
+                              make_pool(eng, ep, n_steps, 4))
     other = None
     if not args.host_loop and not args.no_second_pass:
         # the other input mode, same episode machinery, for comparison
@@ -295,29 +297,39 @@ def run_steps(args, ep, pool, use_graph, world, device):
             "kernel_in_step_ms": sum(a.elapsed_time(b) for a, b in kern) / len(kern)}
 
 
-def kernel_pass(ep, reps=20):
-    """The rollout kernel alone: REPS back-to-back launches on the current
-    controls between two HIP events on the launch stream (events around the
-    single launch inside a step add their own packet overhead)."""
+def kernel_pass(ep, pool, reps=20):
+    """The rollout kernel alone: REPS back-to-back launches between two HIP
+    events on the launch stream, rotating over the resident batches (at least
+    4 x the batch bytes between two uses of a batch, so no launch is served
+    from the 256 MiB Infinity Cache; events around the single launch inside a
+    step would add their own packet overhead)."""
     import torch
     k0 = torch.cuda.Event(enable_timing=True)
     k1 = torch.cuda.Event(enable_timing=True)
+    saved = ep.cur
+    ep.cur = pool[0]
     ep.partials()
     k0.record()
-    for _ in range(reps):
+    for i in range(reps):
+        ep.cur = pool[(i + 1) % len(pool)]
         ep.partials()
     k1.record()
     torch.cuda.synchronize()
+    ep.cur = saved
     return k0.elapsed_time(k1) / reps
 
 
 def roofline(achieved, bytes_launch, traffic_json):
-    traffic = None
+    """traffic: HBM bytes per launch from the committed PMC summary, used only
+    when it was measured on a launch of the same algorithmic size."""
+    traffic, src = None, None
     if traffic_json and os.path.exists(traffic_json):
         with open(traffic_json) as fh:
-            traffic = json.load(fh).get("hbm_bytes_per_launch")
+            t = json.load(fh)
+        if abs(t.get("algorithmic_bytes_per_launch", -1) - bytes_launch) < 1:
+            traffic, src = t.get("hbm_bytes_per_launch"), os.path.relpath(traffic_json, REPO)
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
             "kernel": "k_rollout_argmin", "algorithmic_bytes_per_launch": bytes_launch}
 
 

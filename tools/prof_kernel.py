@@ -1,6 +1,8 @@
-"""Minimal driver for rocprofv3 counter passes: sample one candidate set,
-then launch only the rollout kernel `reps` times.
-    python tools/prof_kernel.py [n_cand] [n_steps] [integ] [reps]"""
+"""Minimal driver for rocprofv3 counter passes: sample B distinct candidate
+batches, then launch only the rollout kernel `reps` times rotating over them
+(B x batch bytes between two uses of a batch > 256 MiB Infinity Cache, so the
+launches stream from HBM as in the bench).
+    python tools/prof_kernel.py [n_cand] [n_steps] [integ] [reps] [batches]"""
 import os
 import sys
 
@@ -17,17 +19,18 @@ from diplomjourney_amd.expansion import Expansion  # noqa: E402
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
     ns = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-    integ = sys.argv[3] if len(sys.argv) > 3 else "rect"
+    integ = sys.argv[3] if len(sys.argv) > 3 else "rect+rot"
     reps = int(sys.argv[4]) if len(sys.argv) > 4 else 20
+    nb = int(sys.argv[5]) if len(sys.argv) > 5 else 4
     eng = Expansion("cuda:0")
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
-    v, b = eng.sample_controls(V, B, n, ns, 7)
+    pool = [eng.sample_controls(V, B, n, ns, 7 + i) for i in range(nb)]
     prob = make_problem(0.0, 0.0, 0.3, 2, 3, 0, 0, 0.5, 0.05, 0.1)
-    for _ in range(reps):
-        eng.partials(prob, v, b, integ)
+    for i in range(reps):
+        eng.partials(prob, *pool[i % nb], integ)
     torch.cuda.synchronize()
-    print("done", n, ns, integ, reps)
+    print("done", n, ns, integ, reps, nb)
 
 
 if __name__ == "__main__":
