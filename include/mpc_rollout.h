@@ -42,7 +42,9 @@ enum {
 /* How the constant integrand of each quad() call is integrated.
  * QK21: bit-faithful emulation of scipy.integrate.quad -> QUADPACK qk21 on a
  *       constant integrand (math_model_tree.py:91-96; SURVEY Fact 4).
- * RECT: the exact integral f*(t_b - t_a) of the constant integrand.        */
+ * RECT: the same integrals of the constant integrands evaluated directly:
+ *       dphi = ((v / L) * h) * tan(beta), x' = fma(v * h, cos(phi'), x),
+ *       h = t_b - t_a (exact integral, fewer roundings; mpc_device.h).   */
 enum { MPC_INTEG_QK21 = 0, MPC_INTEG_RECT = 1 };
 
 /* Flag OR'ed into every `integrator` argument: carry (sin, cos) of the heading
@@ -50,7 +52,8 @@ enum { MPC_INTEG_QK21 = 0, MPC_INTEG_RECT = 1 };
  * evaluating sin/cos of the new heading (math_model_tree.py:113-114) with a
  * full range reduction.  Same mathematics, different rounding (a few ulp on
  * the heading's sin/cos after N steps); ~40% fewer VALU instructions per
- * candidate-step.  Increments |dphi| > 0.25 fall back to direct evaluation. */
+ * candidate-step.  Candidates with an increment |dphi| > 0.2 (or |beta| > 1.1)
+ * are recomputed with direct evaluation. */
 #define MPC_HEADING_ROTATE 0x100
 
 /* One MPC problem (one robot at one MPC step). */
@@ -212,6 +215,41 @@ int mpc_episode_finalize(void* state, const double* v_sc, const double* beta_sc,
                          int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
                          size_t ws_bytes, mpc_result_t* out, const mpc_episode_config_t* advance,
                          mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Full-tree MPC of run_math_model.py / math_model.py.
+ * predictive_control (run_math_model.py:133-228) fills S1^3 leaves, S1 =
+ * |V|*|B|: leaf j = k0*S1^2 + k1*S1 + k2 applies u_k0, u_k1, u_k2 in turn
+ * (u_k = (V[k / |B|], B[k % |B|]), the :158-160 loop order) and is scored with
+ * the heading-term criterion (:82-86)
+ *   10000*dist_target + 10*(arctan(x_t/y_t) - phi)^2 + 100*dist_line^2,
+ * strict < against an incumbent that the reference never resets within an
+ * episode (:193-196).  Leaves are generated from j: nothing per leaf in HBM.
+ * The caller passes arctan(x_t / y_t) as its numpy evaluates it (:83).
+ * ------------------------------------------------------------------------- */
+typedef struct mpc_fulltree_problem {
+  double x, y, phi;           /* initial_coordinates (:139)                     */
+  double x_t, y_t, x_0, y_0;  /* module globals read by the criterion (:56-86)  */
+  double atan_target;         /* arctan(x_t / y_t) (:83)                        */
+  double L, t_a, t_b;         /* quad window [t, t + delta_t] after t += dt      */
+} mpc_fulltree_problem_t;
+
+typedef struct mpc_fulltree_result {
+  double cost;                /* criterion of the best leaf                     */
+  int64_t leaf;               /* j of the first strict minimum, -1 if none      */
+  int32_t found;              /* cost < incumbent                               */
+  int32_t s1;                 /* |V| * |B|                                      */
+  int64_t k[3];               /* control index per layer                        */
+  double v[3], beta[3];       /* the controls                                   */
+  double traj[3][3];          /* layer states (x, y, phi) of the best leaf      */
+} mpc_fulltree_result_t;
+
+size_t mpc_fulltree_workspace_bytes(int32_t n_v, int32_t n_beta);
+/* v_grid / beta_grid: device arrays; out: device pointer. */
+int mpc_fulltree_argmin(const mpc_fulltree_problem_t* p, const double* v_grid, int32_t n_v,
+                        const double* beta_grid, int32_t n_beta, double incumbent,
+                        int32_t integrator, void* ws, size_t ws_bytes,
+                        mpc_fulltree_result_t* out, mpc_stream_t stream);
 
 #ifdef __cplusplus
 }

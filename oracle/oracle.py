@@ -45,6 +45,12 @@ def lib():
         L.mpc_oracle_rollout_argmin_batched.restype = ctypes.c_int
         L.mpc_oracle_rollout_argmin_batched.argtypes = [
             _P, _P, ctypes.c_int32, _P, _P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _P]
+        L.mpc_oracle_fulltree_cost.restype = _D
+        L.mpc_oracle_fulltree_cost.argtypes = [_D] * 8
+        L.mpc_oracle_fulltree_argmin.restype = ctypes.c_int64
+        L.mpc_oracle_fulltree_argmin.argtypes = (
+            [_P, ctypes.c_int32, _P, ctypes.c_int32] + [_D] * 12 + [ctypes.c_int32]
+            + [ctypes.POINTER(_D), ctypes.POINTER(ctypes.c_int32), _P, _P, _P, _P, _P])
         L.mpc_oracle_sample_controls.restype = None
         L.mpc_oracle_sample_controls.argtypes = [
             _P, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
@@ -121,3 +127,32 @@ def sample_controls(v_grid, beta_grid, n_cand, n_steps, seed, index_base=0, cons
                                      n_cand, n_steps, seed, index_base, int(const_prefix),
                                      _ptr(v_sc), _ptr(b_sc), n_cand)
     return v_sc, b_sc
+
+
+def fulltree_cost(x, y, phi, x_t, y_t, x_0, y_0, atan_target):
+    """control_criterion of run_math_model.py:82-86 (heading term)."""
+    return lib().mpc_oracle_fulltree_cost(x, y, phi, x_t, y_t, x_0, y_0, atan_target)
+
+
+def fulltree_argmin(V, B, state, target, origin, atan_target, L, t_a, t_b, incumbent,
+                    integ=MPC_INTEG_QK21, detail=False):
+    """The three layer loops of run_math_model.py:158-197 (S1^3 leaves).
+    Returns dict(leaf, cost, found, traj[3][3]) (+ per-leaf arrays if detail)."""
+    V = np.ascontiguousarray(V, dtype=np.float64)
+    B = np.ascontiguousarray(B, dtype=np.float64)
+    s1 = len(V) * len(B)
+    res = np.zeros(9)
+    arrs = [None] * 4
+    if detail:
+        arrs = [np.zeros(s1 ** 3), np.zeros((s1 ** 3, 3)), np.zeros((s1, 3)),
+                np.zeros((s1 * s1, 3))]
+    best, found = _D(), ctypes.c_int32()
+    leaf = lib().mpc_oracle_fulltree_argmin(
+        _ptr(V), len(V), _ptr(B), len(B), state[0], state[1], state[2], target[0], target[1],
+        origin[0], origin[1], atan_target, L, t_a, t_b, incumbent, _integ(integ),
+        ctypes.byref(best), ctypes.byref(found), _ptr(res), *[_ptr(a) for a in arrs])
+    out = {"leaf": leaf, "cost": best.value, "found": bool(found.value),
+           "traj": res.reshape(3, 3).tolist()}
+    if detail:
+        out.update(costs=arrs[0], leaf_states=arrs[1], layer0=arrs[2], layer1=arrs[3])
+    return out
