@@ -79,7 +79,32 @@ class MpcEpisodeLog(ctypes.Structure):
                     "cost", "x", "y", "phi", "v", "beta")]
 
 
+class MpcFulltreeProblem(ctypes.Structure):
+    """mpc_fulltree_problem_t: one full-tree MPC step (run_math_model.py:133-156)."""
+    _fields_ = [(n, ctypes.c_double) for n in
+                ("x", "y", "phi", "x_t", "y_t", "x_0", "y_0", "atan_target", "L", "t_a",
+                 "t_b")]
+
+
+class MpcFulltreeResult(ctypes.Structure):
+    """mpc_fulltree_result_t: the first strict-minimum leaf and its three layers."""
+    _fields_ = [
+        ("cost", ctypes.c_double),
+        ("leaf", ctypes.c_int64),
+        ("found", ctypes.c_int32),
+        ("s1", ctypes.c_int32),
+        ("k", ctypes.c_int64 * 3),
+        ("v", ctypes.c_double * 3),
+        ("beta", ctypes.c_double * 3),
+        ("traj", (ctypes.c_double * 3) * 3),
+    ]
+
+    def trajectory(self):
+        return [[self.traj[i][k] for k in range(3)] for i in range(3)]
+
+
 RESULT_BYTES = ctypes.sizeof(MpcResult)
+FT_RESULT_BYTES = ctypes.sizeof(MpcFulltreeResult)
 LOG_BYTES = ctypes.sizeof(MpcEpisodeLog)
 PROBLEM_BYTES = ctypes.sizeof(MpcProblem)
 

@@ -1,0 +1,199 @@
+// mpc_fulltree.h — full-tree MPC of run_math_model.py / math_model.py
+// (SURVEY §8f 3): S1^3 leaves per MPC step, generated from the leaf index.
+//
+// predictive_control (run_math_model.py:133-228) fills leaf j = k0*S1^2 +
+// k1*S1 + k2 with the controls u_k0, u_k1, u_k2 (u_k = (V[k / |B|],
+// B[k % |B|]), loop order :158-160) applied in turn to the initial state, and
+// scans the heading-term criterion (:82-86) with strict < against a running
+// incumbent (:193-196).
+//
+//   k_ft_controls   per control k: v, dphi = Q((v/L) tan(beta)) (the same for
+//                   all three layers: one quad window per call), the rotation
+//                   factors of dphi, v*h; a launch-wide flag when some
+//                   |dphi| > kRotMax (the rotation form is then not used)
+//   k_ft_leaves     a wave takes 64 consecutive (k0, k1) pairs (one lane each)
+//                   and a chunk of k2: each lane derives its pair's layer-0 and
+//                   layer-1 states once, then runs the chunk with the control
+//                   of k2 WAVE-UNIFORM (scalar loads, no per-leaf vector
+//                   memory traffic); lexicographic (cost, j) arg-min per lane
+//                   -> wave -> block record
+//   k_ft_finalize   record reduction, the winner's three layers re-derived
+//                   with the same functions
+#pragma once
+
+#include "mpc_kernels.h"
+
+namespace mpc {
+
+struct FtCtl {
+  double v, beta, dphi, sd, cm1;
+};
+
+struct FtState {
+  double x, y, ph, s, c;
+};
+
+// criterion of run_math_model.py:82-86: 10000*dist_target (:64-65)
+// + 10*(arctan(x_t/y_t) - phi)^2 + 100*dist_line^2 (:53-61), in that order.
+MPC_HD __forceinline__ double cost_fulltree(double x, double y, double ph, const Consts& K,
+                                           double atan_t) {
+  const double a = atan_t - ph;
+  const double ex = K.x_t - x, ey = K.y_t - y;
+  const double dist_target = sqrt(ex * ex + ey * ey);
+  double d;
+  if (x == K.x_0 && y == K.y_0) {
+    d = 1000.0;
+  } else {
+    d = fabs(K.A * x - K.B * y + K.C1 - K.C2) / K.den;
+  }
+  return 10000.0 * dist_target + 10.0 * (a * a) + 100.0 * (d * d);
+}
+
+// iteration_of_predict (:111-115) with a precomputed control: heading first,
+// then the position with the new heading.  ROT: (s, c) rotated by the
+// control's factors instead of sin/cos of the new heading.
+template <int INTEG, bool ROT>
+MPC_HD __forceinline__ FtState ft_apply(const FtState& in, const FtCtl& u, const Consts& K) {
+  FtState o;
+  o.ph = in.ph + u.dphi;
+  if constexpr (ROT) {
+    o.s = in.s;
+    o.c = in.c;
+    trig::rotate_by(u.sd, u.cm1, o.s, o.c);
+  } else {
+    trig::sincos_fast(o.ph, &o.s, &o.c);
+  }
+  o.x = position_step<INTEG>(in.x, u.v, o.c, K);
+  o.y = position_step<INTEG>(in.y, u.v, o.s, K);
+  return o;
+}
+
+template <int INTEG>
+__global__ __launch_bounds__(kBlock) void k_ft_controls(Consts K, const double* __restrict__ V,
+                                                        const double* __restrict__ B, int nb,
+                                                        int64_t s1, FtCtl* __restrict__ ctl,
+                                                        uint32_t* __restrict__ no_rot) {
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= s1) return;
+  FtCtl u;
+  u.v = V[k / nb];
+  u.beta = B[k % nb];
+  const double w = K.L_pow2 ? u.v * K.inv_L : u.v / K.L;
+  u.dphi = heading_incr<INTEG>(w, trig::tan_fast(u.beta), K);
+  if (fabs(u.dphi) <= trig::kRotMax) {
+    trig::rotation_factors(u.dphi, u.sd, u.cm1);
+  } else {
+    u.sd = u.cm1 = 0.0;
+    atomicOr(no_rot, 1u);
+  }
+  ctl[k] = u;
+}
+
+constexpr int kFtChunk = 256;  // k2 per wave-item
+
+template <int INTEG, bool ROT>
+__device__ __forceinline__ void ft_leaves_body(const Consts& K, double atan_t,
+                                               const FtCtl* __restrict__ ctl, int64_t s1,
+                                               uint64_t& best_k, int64_t& best_i) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = static_cast<int64_t>(blockIdx.x) * kWaves +
+                       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t n_waves = static_cast<int64_t>(gridDim.x) * kWaves;
+  const int64_t n_pairs = s1 * s1;
+  const int64_t n_groups = (n_pairs + 63) / 64;
+  const int64_t n_chunks = (s1 + kFtChunk - 1) / kFtChunk;
+  const int64_t n_items = n_groups * n_chunks;
+  for (int64_t item = wave; item < n_items; item += n_waves) {
+    const int64_t g = item / n_chunks;
+    const int64_t c = item - g * n_chunks;
+    const int64_t m = g * 64 + lane;           // this lane's (k0, k1) pair
+    const bool live = m < n_pairs;
+    const int64_t mm = live ? m : n_pairs - 1;
+    const int64_t k0 = mm / s1, k1 = mm - k0 * s1;
+    const FtState s0{K.x, K.y, K.phi, K.s0, K.c0};
+    const FtState l0 = ft_apply<INTEG, ROT>(s0, ctl[k0], K);
+    const FtState l1 = ft_apply<INTEG, ROT>(l0, ctl[k1], K);
+    const int64_t k2_lo = c * kFtChunk;
+    const int64_t k2_hi = k2_lo + kFtChunk < s1 ? k2_lo + kFtChunk : s1;
+    const int64_t j0 = mm * s1;
+    for (int64_t k2 = k2_lo; k2 < k2_hi; ++k2) {   // wave-uniform control
+      const FtCtl u = ctl[k2];
+      const FtState lf = ft_apply<INTEG, ROT>(l1, u, K);
+      const uint64_t kk = cost_key(cost_fulltree(lf.x, lf.y, lf.ph, K, atan_t));
+      const int64_t j = j0 + k2;
+      if (live && rec_less(kk, j, best_k, best_i)) {
+        best_k = kk;
+        best_i = j;
+      }
+    }
+  }
+}
+
+template <int INTEG, bool ROT>
+__global__ __launch_bounds__(kBlock) void k_ft_leaves(Consts K, double atan_t,
+                                                      const FtCtl* __restrict__ ctl,
+                                                      const uint32_t* __restrict__ no_rot,
+                                                      int64_t s1, Rec* __restrict__ part) {
+  uint64_t best_k = ~0ull;
+  int64_t best_i = INT64_MAX;
+  if (ROT && *no_rot == 0u)
+    ft_leaves_body<INTEG, true>(K, atan_t, ctl, s1, best_k, best_i);
+  else
+    ft_leaves_body<INTEG, false>(K, atan_t, ctl, s1, best_k, best_i);
+  block_argmin(best_k, best_i);
+  if (threadIdx.x == 0) part[blockIdx.x] = Rec{best_k, best_i};
+}
+
+template <int INTEG, bool ROT>
+__global__ __launch_bounds__(kFinBlock) void k_ft_finalize(
+    const Rec* __restrict__ part, int n_part, Consts K, const FtCtl* __restrict__ ctl,
+    const uint32_t* __restrict__ no_rot, int64_t s1, double incumbent,
+    mpc_fulltree_result_t* __restrict__ out) {
+  __shared__ uint64_t s_key[kFinBlock / 64];
+  __shared__ int64_t s_idx[kFinBlock / 64];
+  uint64_t k = ~0ull;
+  int64_t i = INT64_MAX;
+  for (int p = threadIdx.x; p < n_part; p += kFinBlock)
+    if (rec_less(part[p].key, part[p].idx, k, i)) {
+      k = part[p].key;
+      i = part[p].idx;
+    }
+  wave_argmin(k, i);
+  if ((threadIdx.x & 63) == 0) {
+    s_key[threadIdx.x >> 6] = k;
+    s_idx[threadIdx.x >> 6] = i;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  for (int w = 1; w < kFinBlock / 64; ++w)
+    if (rec_less(s_key[w], s_idx[w], k, i)) {
+      k = s_key[w];
+      i = s_idx[w];
+    }
+  out->s1 = static_cast<int32_t>(s1);
+  if (k == ~0ull) {
+    out->cost = __builtin_inf();
+    out->leaf = -1;
+    out->found = 0;
+    return;
+  }
+  const double c = key_cost(k);
+  out->cost = c;
+  out->leaf = i;
+  out->found = c < incumbent ? 1 : 0;
+  const int64_t kk[3] = {i / (s1 * s1), (i / s1) % s1, i % s1};
+  const bool rot = ROT && *no_rot == 0u;
+  FtState st{K.x, K.y, K.phi, K.s0, K.c0};
+  for (int l = 0; l < 3; ++l) {
+    const FtCtl u = ctl[kk[l]];
+    st = rot ? ft_apply<INTEG, true>(st, u, K) : ft_apply<INTEG, false>(st, u, K);
+    out->k[l] = kk[l];
+    out->v[l] = u.v;
+    out->beta[l] = u.beta;
+    out->traj[l][0] = st.x;
+    out->traj[l][1] = st.y;
+    out->traj[l][2] = st.ph;
+  }
+}
+
+}  // namespace mpc

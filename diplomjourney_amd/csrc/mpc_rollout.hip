@@ -16,6 +16,7 @@
 
 #include "../../include/mpc_rollout.h"
 #include "mpc_episode.h"
+#include "mpc_fulltree.h"
 #include "mpc_kernels.h"
 
 namespace mpc {
@@ -443,6 +444,57 @@ int mpc_episode_advance(const mpc_episode_config_t* cfg, void* state, const mpc_
     return MPC_ERR_ARG;
   k_episode_advance<<<1, 64, 0, reinterpret_cast<hipStream_t>(stream)>>>(
       *cfg, static_cast<EpisodeState*>(state), results, n_results, log, log_capacity);
+  return last_hip_status();
+}
+
+// ----------------------------- full tree -----------------------------------
+static size_t ft_align(size_t n) { return (n + 255) & ~static_cast<size_t>(255); }
+static constexpr int64_t kFtMaxBlocks = 2048;
+
+size_t mpc_fulltree_workspace_bytes(int32_t n_v, int32_t n_beta) {
+  if (n_v < 1 || n_beta < 1) return 0;
+  const size_t s1 = static_cast<size_t>(n_v) * static_cast<size_t>(n_beta);
+  return ft_align(s1 * sizeof(FtCtl)) + 256 + kFtMaxBlocks * sizeof(Rec);
+}
+
+int mpc_fulltree_argmin(const mpc_fulltree_problem_t* p, const double* v_grid, int32_t n_v,
+                        const double* beta_grid, int32_t n_beta, double incumbent,
+                        int32_t integrator, void* ws, size_t ws_bytes,
+                        mpc_fulltree_result_t* out, mpc_stream_t stream) {
+  if (!p || !v_grid || !beta_grid || !out || n_v < 1 || n_beta < 1) return MPC_ERR_ARG;
+  const int64_t s1 = static_cast<int64_t>(n_v) * n_beta;
+  if (s1 > 2000000) return MPC_ERR_ARG;  // S1^3 must fit int64 leaf indices
+  if (mode_ok(integrator) != MPC_OK) return MPC_ERR_UNSUPPORTED;
+  if (!ws || ws_bytes < mpc_fulltree_workspace_bytes(n_v, n_beta)) return MPC_ERR_WORKSPACE;
+  mpc_problem_t q;
+  q.x = p->x;
+  q.y = p->y;
+  q.phi = p->phi;
+  q.x_t = p->x_t;
+  q.y_t = p->y_t;
+  q.x_0 = p->x_0;
+  q.y_0 = p->y_0;
+  q.L = p->L;
+  q.t_a = p->t_a;
+  q.t_b = p->t_b;
+  const Consts K = host_consts(q);
+  char* w = static_cast<char*>(ws);
+  FtCtl* ctl = reinterpret_cast<FtCtl*>(w);
+  uint32_t* no_rot = reinterpret_cast<uint32_t*>(w + ft_align(s1 * sizeof(FtCtl)));
+  Rec* part = reinterpret_cast<Rec*>(w + ft_align(s1 * sizeof(FtCtl)) + 256);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(no_rot, 0, sizeof(uint32_t), st) != hipSuccess) return MPC_ERR_HIP;
+  const int64_t n_items = cdiv(s1 * s1, 64) * cdiv(s1, kFtChunk);
+  const int64_t grid = std::max<int64_t>(1, std::min(cdiv(n_items, kWaves), kFtMaxBlocks));
+  dispatch_mode(integrator, [&](auto integ, auto rot) {
+    constexpr int I = decltype(integ)::value;
+    constexpr bool R = decltype(rot)::value;
+    k_ft_controls<I><<<cdiv(s1, kBlock), kBlock, 0, st>>>(K, v_grid, beta_grid, n_beta, s1, ctl,
+                                                          no_rot);
+    k_ft_leaves<I, R><<<grid, kBlock, 0, st>>>(K, p->atan_target, ctl, no_rot, s1, part);
+    k_ft_finalize<I, R><<<1, kFinBlock, 0, st>>>(part, static_cast<int>(grid), K, ctl, no_rot,
+                                                 s1, incumbent, out);
+  });
   return last_hip_status();
 }
 

@@ -12,7 +12,7 @@ import os
 import subprocess
 import sys
 
-from .abi import MpcEpisodeConfig, MpcError, MpcProblem
+from .abi import MpcEpisodeConfig, MpcError, MpcFulltreeProblem, MpcProblem
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
@@ -31,6 +31,7 @@ EXPORTS = (
     "mpc_sample_controls", "mpc_episode_state_bytes", "mpc_episode_reset",
     "mpc_episode_expand", "mpc_episode_advance", "mpc_episode_sample", "mpc_episode_partials",
     "mpc_episode_finalize", "mpc_episode_rollout",
+    "mpc_fulltree_workspace_bytes", "mpc_fulltree_argmin",
 )
 
 HIPCC_FLAGS = [
@@ -121,6 +122,11 @@ def lib():
     L.mpc_episode_finalize.restype = ctypes.c_int
     L.mpc_episode_finalize.argtypes = [_P, _P, _P, _I64, _I32, _I64, _I32, _P, ctypes.c_size_t,
                                        _P, ctypes.POINTER(MpcEpisodeConfig), _P, _I32, _P]
+    L.mpc_fulltree_workspace_bytes.restype = ctypes.c_size_t
+    L.mpc_fulltree_workspace_bytes.argtypes = [_I32, _I32]
+    L.mpc_fulltree_argmin.restype = ctypes.c_int
+    L.mpc_fulltree_argmin.argtypes = [ctypes.POINTER(MpcFulltreeProblem), _P, _I32, _P, _I32,
+                                      ctypes.c_double, _I32, _P, ctypes.c_size_t, _P, _P]
     L.mpc_episode_rollout.restype = ctypes.c_int
     L.mpc_episode_rollout.argtypes = [_P, _P, _P, _I64, _I32, _I64, _I32, _P, ctypes.c_size_t,
                                       _P, ctypes.POINTER(MpcEpisodeConfig), _P, _I32, _P]

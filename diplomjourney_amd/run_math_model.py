@@ -1,0 +1,186 @@
+"""Drop-in for run_math_model.py's full-tree MPC on MI355X.
+
+Same module surface as the reference script's definitions
+(run_math_model.py:1-229): the grids `vector_v` / `vector_beta` (:24-33), the
+module globals read by the criterion (`x_0, y_0, x_t, y_t, t`,
+`optimal_criterion`, `optimal_trajectory`), `is_on_target`,
+`get_distance_from_line`, `get_distance_from_target`, `saturation`,
+`control_criterion` and `predictive_control(_initial_x, _initial_y,
+_initial_phi, _initial_velocity, _target_x, _target_y)` with the same return
+value.  `predictive_control` evaluates all S1^3 leaves of the tree in ONE
+C-ABI call (`mpc_fulltree_argmin`, include/mpc_rollout.h) instead of the
+three Python layer loops (:158-197), keeping the reference's incumbent rule:
+`optimal_criterion` is NOT reset between calls of an episode (:193-196), and
+when no leaf beats it the previous winner's first-layer state is returned
+again (the reference re-reads its stale `optimal_trajectory`).
+
+`run_episode` re-enacts one iteration of the script's episode loop
+(:231-280) without the plotting; `configure(delta_v, delta_beta)` rebuilds
+the grids for a different control resolution (at the reference's config the
+tree has S1^3 = 1.4e13 leaves, SURVEY Fact 2).
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import config as _cfg
+from .abi import MpcFulltreeProblem
+from .expansion import Expansion, fulltree_argmin, fulltree_result
+
+L = _cfg.L
+delta_t = _cfg.delta_t
+beta_max = _cfg.beta_max
+v_max = _cfg.v_max
+eps = _cfg.eps
+
+# Actual (:13-19)
+beta = 0
+v = 0
+phi = _cfg.phi_0
+x = _cfg.x_0
+y = _cfg.y_0
+x_0, y_0, phi_0 = _cfg.x_0, _cfg.y_0, _cfg.phi_0
+x_t, y_t = _cfg.x_t, _cfg.y_t
+
+prediction_horizon = 3
+INTEGRATOR = "qk21"        # the reference's quad() arithmetic; "rect", "+rot" as in the ABI
+
+vector_v = vector_beta = None
+size_max_1 = size_max_2 = size_max_3 = 0
+t = 0
+optimal_trajectory = [0]
+optimal_criterion = None
+
+_engine = None
+_grids_dev = None
+
+
+def configure(delta_v=_cfg.delta_v, delta_beta=_cfg.delta_beta):
+    """The grids of :24-33 for a control resolution (defaults: config.py)."""
+    global vector_v, vector_beta, size_max_1, size_max_2, size_max_3, _grids_dev
+    vector_v = np.round(np.arange(0, v_max + delta_v, delta_v), 3)   # v = 0 at import (:14)
+    vector_beta = np.round(np.arange(-beta_max, beta_max + delta_beta, delta_beta), 3)
+    size_max_1 = np.size(vector_beta) * np.size(vector_v)
+    size_max_2 = pow(size_max_1, 2)
+    size_max_3 = pow(size_max_1, 3)
+    _grids_dev = None
+
+
+configure()
+
+
+def is_on_target(actual_x, actual_y, target_x, target_y):
+    return (target_x - actual_x) ** 2 + (target_y - actual_y) ** 2 <= eps
+
+
+def get_distance_from_line(x_a, y_a):
+    if x_a == x_0 and y_a == y_0:
+        return 1000
+    return (abs((y_t - y_0) * x_a - (x_t - x_0) * y_a + x_t * y_0 - y_t * x_0)
+            / (math.sqrt((y_t - y_0) ** 2 + (x_t - x_0) ** 2)))
+
+
+def get_distance_from_target(x_a, y_a):
+    return math.sqrt((x_t - x_a) ** 2 + (y_t - y_a) ** 2)
+
+
+def saturation(value, value_mplt):
+    if value > value_mplt:
+        value = value_mplt
+    elif value < -value_mplt:
+        value = -value_mplt
+    return value
+
+
+def control_criterion(predicted_coordinates):
+    """:82-86, host scalar (the episode's first incumbent); the leaves are
+    scored on the device by the same expression (csrc/mpc_fulltree.h)."""
+    angle_from_line = (np.arctan(x_t / y_t) - predicted_coordinates[2])
+    distance_from_target = get_distance_from_target(predicted_coordinates[0],
+                                                    predicted_coordinates[1])
+    distance_from_line = get_distance_from_line(predicted_coordinates[0],
+                                                predicted_coordinates[1])
+    return 10000 * distance_from_target + 10 * angle_from_line ** 2 + 100 * distance_from_line ** 2
+
+
+def _device():
+    global _engine, _grids_dev
+    if _engine is None:
+        _engine = Expansion("cuda")
+    if _grids_dev is None:
+        _grids_dev = (torch.tensor(np.asarray(vector_v, dtype=np.float64), device=_engine.device),
+                      torch.tensor(np.asarray(vector_beta, dtype=np.float64),
+                                   device=_engine.device))
+    return _engine, _grids_dev
+
+
+def predictive_control(_initial_x, _initial_y, _initial_phi, _initial_velocity, _target_x,
+                       _target_y):
+    """:133-228 — one MPC step over the full tree; returns [x, y, phi, v, beta]
+    of the best leaf's first layer.  (_initial_velocity, _target_* are unused
+    by the reference's expansion as well.)"""
+    global optimal_trajectory, optimal_criterion, t
+    t += delta_t                                                   # :156
+    eng, (vg, bg) = _device()
+    p = MpcFulltreeProblem(float(_initial_x), float(_initial_y), float(_initial_phi),
+                           float(x_t), float(y_t), float(x_0), float(y_0),
+                           float(np.arctan(x_t / y_t)), float(L), float(t),
+                           float(t + delta_t))
+    r = fulltree_result(fulltree_argmin(eng, p, vg, bg, optimal_criterion, INTEGRATOR))
+    if r.found:
+        optimal_criterion = r.cost
+        optimal_trajectory = [[r.trajectory()[i] + ([r.v[0], r.beta[0]] if i == 0 else [])
+                               for i in range(3)]]
+    # the reference reads optimal_trajectory[0][0] whether or not it changed
+    # (an int 0 before any winner: the same TypeError as the script)
+    first = optimal_trajectory[0][0]
+    return [first[0], first[1], first[2], first[3], first[4]]
+
+
+def start_episode(x0, y0, phi0, xt, yt):
+    """The per-episode resets of :232-246 (plotting omitted)."""
+    global t, v, x_0, y_0, phi_0, x_t, y_t, x, y, phi, optimal_trajectory, optimal_criterion
+    t = 0
+    v = 0
+    x_0, y_0, phi_0, x_t, y_t = x0, y0, phi0, xt, yt
+    x, y, phi = x_0, y_0, phi_0
+    optimal_trajectory = [0]
+    optimal_criterion = control_criterion([x_0, y_0, phi_0])
+
+
+def run_episode(seed=None, max_calls=None):
+    """One iteration of the :231-280 episode loop: random start and target
+    from numpy's global RNG (seeded here when `seed` is given), MPC steps until
+    on target, two non-moves ("Recursive error", :267-270) or `max_calls`.
+    Returns (records, stop) with one (x, y, phi, v) -> result record per step."""
+    global x, y, phi, v, beta
+    if seed is not None:
+        np.random.seed(seed)
+    x0 = np.random.uniform(-10, 10)
+    y0 = np.random.uniform(-10, 10)
+    phi0 = np.random.uniform(-math.pi, math.pi)
+    xt = np.random.uniform(x0 - 10, x0 + 10)
+    yt = np.random.uniform(y0 - 10, y0 + 10)
+    start_episode(x0, y0, phi0, xt, yt)
+    k = 0
+    x_previous, y_previous = x, y
+    records = []
+    while not is_on_target(x, y, x_t, y_t):
+        if max_calls is not None and len(records) == max_calls:
+            return records, "max_calls"
+        pre = (x, y, phi, v, t, optimal_criterion)
+        coordinates = predictive_control(x, y, phi, v, x_t, y_t)
+        records.append({"pre": pre, "ret": coordinates, "optimal_criterion": optimal_criterion})
+        x, y, phi, v, beta = coordinates
+        if x == x_previous and y == y_previous:
+            k += 1
+        if k == 2:
+            return records, "recursive_error"
+        x_previous, y_previous = x, y
+    return records, "on_target"
+
+
+__all__ = ["configure", "is_on_target", "get_distance_from_line", "get_distance_from_target",
+           "saturation", "control_criterion", "predictive_control", "start_episode",
+           "run_episode", "prediction_horizon"]

@@ -1,0 +1,107 @@
+"""Full-tree MPC on the GPU (mpc_fulltree_argmin, csrc/mpc_fulltree.h) against
+the CPU oracle and the reference fixtures (tests/golden/fulltree_reference.json)."""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                    "fulltree_reference.json")
+STATE_TOL = 1e-9
+COST_RTOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def gold():
+    with open(GOLD) as fh:
+        return json.load(fh)
+
+
+def _device_call(engine, V, B, state, target, origin, atan_t, L, t_a, t_b, inc, integ):
+    from diplomjourney_amd.abi import MpcFulltreeProblem
+    from diplomjourney_amd.expansion import fulltree_argmin, fulltree_result
+    vg = torch.tensor(V, dtype=torch.float64, device=engine.device)
+    bg = torch.tensor(B, dtype=torch.float64, device=engine.device)
+    p = MpcFulltreeProblem(*state, *target, *origin, atan_t, L, t_a, t_b)
+    return fulltree_result(fulltree_argmin(engine, p, vg, bg, inc, integ))
+
+
+def _agree(dev, ref):
+    if dev.leaf != ref["leaf"]:
+        # only an exact-arithmetic near-tie may flip the winner
+        assert abs(dev.cost - ref["cost"]) <= 1e-13 * abs(ref["cost"]), (dev.leaf, ref["leaf"])
+        return
+    assert math.isclose(dev.cost, ref["cost"], rel_tol=COST_RTOL)
+    assert bool(dev.found) == ref["found"]
+    assert max(abs(a - b) for a, b in zip(sum(dev.trajectory(), []), sum(ref["traj"], [])))\
+        <= STATE_TOL
+
+
+@pytest.mark.parametrize("integ", ["qk21", "rect", "qk21+rot", "rect+rot"])
+def test_random_problems_vs_oracle(engine, integ):
+    """S1 = 8 x 9 = 72 (373,248 leaves) on 6 random problems per mode."""
+    rng = np.random.default_rng(5)
+    V = np.round(np.arange(0.0, 1.0 + 0.125, 0.125), 3)[:8]
+    B = np.round(np.linspace(-1.047, 1.047, 9), 3)
+    for _ in range(6):
+        st = (float(rng.uniform(-5, 5)), float(rng.uniform(-5, 5)), float(rng.uniform(-3, 3)))
+        tg = (float(rng.uniform(-8, 8)), float(rng.uniform(-8, 8)))
+        org = (float(rng.uniform(-3, 3)), float(rng.uniform(-3, 3)))
+        atan_t = float(np.arctan(tg[0] / tg[1]))
+        t_a = float(rng.integers(1, 40)) * 0.05
+        ref = O.fulltree_argmin(V, B, st, tg, org, atan_t, 0.5, t_a, t_a + 0.05, 1e18,
+                                integ=integ)
+        dev = _device_call(engine, V, B, st, tg, org, atan_t, 0.5, t_a, t_a + 0.05, 1e18, integ)
+        _agree(dev, ref)
+        assert dev.s1 == 72 and dev.found == 1
+
+
+def test_reference_detail_call(engine, gold):
+    """The first recorded reference call (15625 leaves): same winner as the
+    reference scan, same cost and states."""
+    cfg, det = gold["config"], gold["detail"]
+    ep = gold["episodes"][det["episode"]]
+    call = ep["calls"][det["call"]]
+    t_a = call["pre"]["t"] + cfg["delta_t"]
+    costs = np.array(det["leaf_costs"])
+    inc = call["pre"]["optimal_criterion"]
+    want = int(np.argmin(costs))                 # first index of the minimum
+    dev = _device_call(engine, gold["vector_v"], gold["vector_beta"],
+                       (call["x"], call["y"], call["phi"]), (ep["x_t"], ep["y_t"]),
+                       (ep["x_0"], ep["y_0"]), float(np.arctan(ep["x_t"] / ep["y_t"])),
+                       cfg["L"], t_a, t_a + cfg["delta_t"], inc, "qk21")
+    assert dev.leaf == want and dev.found == 1
+    assert math.isclose(dev.cost, costs[want], rel_tol=COST_RTOL)
+    assert max(abs(a - b) for a, b in zip(dev.trajectory()[2],
+                                          det["leaf_states_last_layer"][want])) <= STATE_TOL
+
+
+def test_drop_in_episodes(engine, gold):
+    """diplomjourney_amd.run_math_model replays the three reference episodes
+    (same seeds, same RNG draws, same stop rule) at the fixtures' grid."""
+    from diplomjourney_amd import run_math_model as rmm
+    cfg = gold["config"]
+    rmm.configure(cfg["delta_v"], cfg["delta_beta"])
+    try:
+        assert list(rmm.vector_v) == gold["vector_v"]
+        assert list(rmm.vector_beta) == gold["vector_beta"]
+        for ep in gold["episodes"]:
+            recs, stop = rmm.run_episode(ep["seed"], max_calls=6)
+            assert (rmm.x_0, rmm.y_0, rmm.phi_0, rmm.x_t, rmm.y_t) == \
+                (ep["x_0"], ep["y_0"], ep["phi_0"], ep["x_t"], ep["y_t"])
+            assert stop == ep["stop"] and len(recs) == len(ep["calls"])
+            assert recs[0]["pre"][5] == ep["first_incumbent"]
+            for r, c in zip(recs, ep["calls"]):
+                assert r["ret"][3:] == c["ret"][3:]                       # chosen v, beta
+                assert max(abs(a - b) for a, b in zip(r["ret"][:3], c["ret"][:3])) <= STATE_TOL
+                assert math.isclose(r["optimal_criterion"], c["post"]["optimal_criterion"],
+                                    rel_tol=COST_RTOL)
+    finally:
+        rmm.configure()
