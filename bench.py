@@ -57,7 +57,16 @@ WORKLOADS = {
               desc="config D: N=12, 1.25e6 candidates/GPU (1e7 at 8 GPUs), RCCL exchange"),
     "E": dict(n_steps=8, per_gpu=None, robots=1024, cand=10_000,
               desc="config E: 1024 robots x 1e4 candidates, N=8, batched per-robot arg-min"),
+    "F": dict(n_steps=3, per_gpu=None,
+              desc="full tree of run_math_model.py (SURVEY 8f 3): S1 = 11 x 41 controls, "
+                   "S1^3 = 9.17e7 leaves per MPC step, heading-term criterion, never-reset "
+                   "incumbent; episode of the run_math_model drop-in"),
 }
+FP64_VECTOR_PEAK_TFLOPS = 78.6   # MI355X spec (2 x 32 lanes x 2 flops/clk/SIMD at 2.4 GHz / 2)
+# fp64 operations per full-tree leaf (csrc/mpc_fulltree.h, one layer step + criterion), as
+# written: rect+rot 34 (heading add 1, rotation 8, two fused position updates 4, criterion 21);
+# qk21 adds 2 x 22 per leaf (two 21-node Kronrod sums + scaling).
+FT_FLOPS_PER_LEAF = {"rect+rot": 34, "rect": 34, "qk21+rot": 78, "qk21": 78}
 
 
 def parse():
@@ -95,6 +104,26 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_baseline_fulltree(seconds):
+    """Config F: the C oracle of the full tree (oracle/mpc_oracle.c, qk21 and
+    glibc trig as the reference) on one host core, S1 = 6 x 11 trees."""
+    import math as _m
+    import numpy as np
+    from oracle import oracle as O
+    V = np.round(np.arange(0, 1 + 0.2, 0.2), 3)
+    B = np.round(np.linspace(-1.047, 1.047, 11), 3)
+    n, leaves, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        O.fulltree_argmin(V, B, (0.1 * n, 0.0, 0.3), (4.0, 5.0), (0.0, 0.0),
+                          float(np.arctan(4.0 / 5.0)), 0.5, 0.05, 0.1, 1e18)
+        n += 1
+        leaves += (len(V) * len(B)) ** 3
+    dt = time.perf_counter() - t0
+    return {"value": leaves / dt, "unit": "leaves/s", "cores": 1, "kind": "port",
+            "sample": f"{n} full trees of S1 = {len(V) * len(B)} ({leaves} leaves), C oracle "
+                      f"(qk21, glibc trig), {dt:.1f} s"}
+
+
 def cpu_baseline(wl, seconds):
     """Reference-structured Python port on host cores (before GPU init)."""
     import numpy as np
@@ -123,7 +152,8 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(wl, args.cpu_seconds)
+        cpu = (cpu_baseline_fulltree(args.cpu_seconds) if args.workload == "F"
+               else cpu_baseline(wl, args.cpu_seconds))
 
     import torch
     import torch.distributed as dist
@@ -141,6 +171,8 @@ def main():
 
     if args.workload == "E":
         return bench_robots(args, wl, eng, rank, world, cpu)
+    if args.workload == "F":
+        return bench_fulltree(args, wl, eng, rank, world, cpu)
 
     from diplomjourney_amd.episode import DeviceEpisode, Episode, percentile
     n_total = (args.candidates_per_gpu or wl["per_gpu"]) * world
@@ -416,6 +448,70 @@ def bench_robots(args, wl, eng, rank, world, cpu):
     }
     if rank == 0:
         print(json.dumps(outd), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_fulltree(args, wl, eng, rank, world, cpu):
+    """Config F: the run_math_model full tree; one mpc_fulltree_argmin per MPC
+    step inside the drop-in's episode (host reads the 200-B result each step,
+    as predictive_control returns it).  G > 1: independent replicas (each rank
+    runs its own episode; the full tree is not sharded in round 1)."""
+    import math as _m
+    import torch
+    import torch.distributed as dist
+    from diplomjourney_amd import run_math_model as rmm
+    from diplomjourney_amd.episode import percentile
+    rmm.INTEGRATOR = args.integrator
+    rmm.configure(0.1, _m.radians(3))
+    s1 = int(rmm.size_max_1)
+    leaves = s1 ** 3
+    rmm.start_episode(-3.0, -2.0, 0.3, 4.0, 5.0)
+
+    def step():
+        c = rmm.predictive_control(rmm.x, rmm.y, rmm.phi, rmm.v, rmm.x_t, rmm.y_t)
+        rmm.x, rmm.y, rmm.phi, rmm.v, rmm.beta = c
+
+    for _ in range(args.warmup):
+        step()
+    ms = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        a = time.perf_counter()
+        step()
+        ms.append((time.perf_counter() - a) * 1e3)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=eng.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    per_step = elapsed / args.steps
+    flops = FT_FLOPS_PER_LEAF[args.integrator] * leaves / per_step
+    out = {
+        "metric": METRIC, "value": world * leaves * args.steps / elapsed, "unit": "leaves/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": per_step * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": wl["desc"], "s1": s1, "leaves_per_step": leaves,
+                   "integrator": args.integrator,
+                   "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
+        "p50_ms": percentile(ms, 50),
+        "roofline": {"bound": "valu-fp64", "achieved": flops / 1e12,
+                     "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": flops / 1e12 / FP64_VECTOR_PEAK_TFLOPS, "traffic": None,
+                     "kernel": "k_ft_leaves",
+                     "note": "algorithmic fp64 ops per leaf as written (FT_FLOPS_PER_LEAF); "
+                             "leaves are generated from the index, no HBM stream"},
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
