@@ -11,8 +11,9 @@
 //                   all three layers: one quad window per call), the rotation
 //                   factors of dphi, v*h; a launch-wide flag when some
 //                   |dphi| > kRotMax (the rotation form is then not used)
-//   k_ft_leaves     a wave takes 64 consecutive (k0, k1) pairs (one lane each)
-//                   and a chunk of k2: each lane derives its pair's layer-0 and
+//   k_ft_leaves     work items = (64 consecutive (k0, k1) pairs, chunk of k2);
+//                   a shard owns a contiguous item range.  A wave takes an
+//                   item, one pair per lane: each lane derives its pair's layer-0 and
 //                   layer-1 states once, then runs the chunk with the control
 //                   of k2 WAVE-UNIFORM (scalar loads, no per-leaf vector
 //                   memory traffic); lexicographic (cost, j) arg-min per lane
@@ -94,16 +95,15 @@ constexpr int kFtChunk = 256;  // k2 per wave-item
 template <int INTEG, bool ROT>
 __device__ __forceinline__ void ft_leaves_body(const Consts& K, double atan_t,
                                                const FtCtl* __restrict__ ctl, int64_t s1,
+                                               int64_t item_lo, int64_t item_hi,
                                                uint64_t& best_k, int64_t& best_i) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = static_cast<int64_t>(blockIdx.x) * kWaves +
                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t n_waves = static_cast<int64_t>(gridDim.x) * kWaves;
   const int64_t n_pairs = s1 * s1;
-  const int64_t n_groups = (n_pairs + 63) / 64;
   const int64_t n_chunks = (s1 + kFtChunk - 1) / kFtChunk;
-  const int64_t n_items = n_groups * n_chunks;
-  for (int64_t item = wave; item < n_items; item += n_waves) {
+  for (int64_t item = item_lo + wave; item < item_hi; item += n_waves) {
     const int64_t g = item / n_chunks;
     const int64_t c = item - g * n_chunks;
     const int64_t m = g * 64 + lane;           // this lane's (k0, k1) pair
@@ -133,13 +133,14 @@ template <int INTEG, bool ROT>
 __global__ __launch_bounds__(kBlock) void k_ft_leaves(Consts K, double atan_t,
                                                       const FtCtl* __restrict__ ctl,
                                                       const uint32_t* __restrict__ no_rot,
-                                                      int64_t s1, Rec* __restrict__ part) {
+                                                      int64_t s1, int64_t item_lo,
+                                                      int64_t item_hi, Rec* __restrict__ part) {
   uint64_t best_k = ~0ull;
   int64_t best_i = INT64_MAX;
   if (ROT && *no_rot == 0u)
-    ft_leaves_body<INTEG, true>(K, atan_t, ctl, s1, best_k, best_i);
+    ft_leaves_body<INTEG, true>(K, atan_t, ctl, s1, item_lo, item_hi, best_k, best_i);
   else
-    ft_leaves_body<INTEG, false>(K, atan_t, ctl, s1, best_k, best_i);
+    ft_leaves_body<INTEG, false>(K, atan_t, ctl, s1, item_lo, item_hi, best_k, best_i);
   block_argmin(best_k, best_i);
   if (threadIdx.x == 0) part[blockIdx.x] = Rec{best_k, best_i};
 }

@@ -459,9 +459,10 @@ size_t mpc_fulltree_workspace_bytes(int32_t n_v, int32_t n_beta) {
 
 int mpc_fulltree_argmin(const mpc_fulltree_problem_t* p, const double* v_grid, int32_t n_v,
                         const double* beta_grid, int32_t n_beta, double incumbent,
-                        int32_t integrator, void* ws, size_t ws_bytes,
-                        mpc_fulltree_result_t* out, mpc_stream_t stream) {
+                        int32_t integrator, int32_t shard, int32_t n_shards, void* ws,
+                        size_t ws_bytes, mpc_fulltree_result_t* out, mpc_stream_t stream) {
   if (!p || !v_grid || !beta_grid || !out || n_v < 1 || n_beta < 1) return MPC_ERR_ARG;
+  if (n_shards < 1 || shard < 0 || shard >= n_shards) return MPC_ERR_ARG;
   const int64_t s1 = static_cast<int64_t>(n_v) * n_beta;
   if (s1 > 2000000) return MPC_ERR_ARG;  // S1^3 must fit int64 leaf indices
   if (mode_ok(integrator) != MPC_OK) return MPC_ERR_UNSUPPORTED;
@@ -485,13 +486,18 @@ int mpc_fulltree_argmin(const mpc_fulltree_problem_t* p, const double* v_grid, i
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (hipMemsetAsync(no_rot, 0, sizeof(uint32_t), st) != hipSuccess) return MPC_ERR_HIP;
   const int64_t n_items = cdiv(s1 * s1, 64) * cdiv(s1, kFtChunk);
-  const int64_t grid = std::max<int64_t>(1, std::min(cdiv(n_items, kWaves), kFtMaxBlocks));
+  const int64_t base = n_items / n_shards, rem = n_items % n_shards;
+  const int64_t item_lo = shard * base + std::min<int64_t>(shard, rem);
+  const int64_t item_hi = item_lo + base + (shard < rem ? 1 : 0);
+  const int64_t grid =
+      std::max<int64_t>(1, std::min(cdiv(item_hi - item_lo, kWaves), kFtMaxBlocks));
   dispatch_mode(integrator, [&](auto integ, auto rot) {
     constexpr int I = decltype(integ)::value;
     constexpr bool R = decltype(rot)::value;
     k_ft_controls<I><<<cdiv(s1, kBlock), kBlock, 0, st>>>(K, v_grid, beta_grid, n_beta, s1, ctl,
                                                           no_rot);
-    k_ft_leaves<I, R><<<grid, kBlock, 0, st>>>(K, p->atan_target, ctl, no_rot, s1, part);
+    k_ft_leaves<I, R><<<grid, kBlock, 0, st>>>(K, p->atan_target, ctl, no_rot, s1, item_lo,
+                                                item_hi, part);
     k_ft_finalize<I, R><<<1, kFinBlock, 0, st>>>(part, static_cast<int>(grid), K, ctl, no_rot,
                                                  s1, incumbent, out);
   });

@@ -67,3 +67,35 @@ def exchange_winner(engine, local_out, incumbent=math.inf, group=None):
     """Device path: all_gather (RCCL) + on-device selection into engine.result."""
     gathered = gather_results(local_out, group)
     return engine.select_winner(gathered, incumbent=incumbent)
+
+
+def select_fulltree(records, incumbent=math.inf):
+    """Winner over the per-shard full-tree results (MpcFulltreeResult list or
+    the all_gather'ed bytes): lexicographic (cost, global leaf) minimum, as
+    the reference's single scan over j; `found` against the incumbent."""
+    from .abi import FT_RESULT_BYTES, MpcFulltreeResult
+    if isinstance(records, (bytes, bytearray, memoryview)):
+        raw = bytes(records)
+        records = [MpcFulltreeResult.from_buffer_copy(raw[i:i + FT_RESULT_BYTES])
+                   for i in range(0, len(raw), FT_RESULT_BYTES)]
+
+    def key(r):
+        if r.leaf < 0 or not (r.cost < math.inf):
+            return (1, 0.0, 0)
+        return (0, r.cost + 0.0, r.leaf)
+
+    best = min(records, key=key)
+    out = MpcFulltreeResult.from_buffer_copy(bytes(best))
+    out.found = int(key(out)[0] == 0 and out.cost < incumbent)
+    return out
+
+
+def gather_bytes(local, group=None):
+    """all_gather of one uint8 record per rank (RCCL on device tensors; gloo
+    groups stage through host memory) -> uint8[world * len]."""
+    world = dist.get_world_size(group)
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        return gather_bytes(local.cpu(), group).to(local.device)
+    out = torch.empty(world * local.numel(), dtype=torch.uint8, device=local.device)
+    dist.all_gather_into_tensor(out, local, group=group)
+    return out

@@ -161,10 +161,12 @@ class Expansion:
         return v_out, beta_out
 
 
-def fulltree_argmin(engine, problem, v_grid, beta_grid, incumbent, integrator="qk21"):
+def fulltree_argmin(engine, problem, v_grid, beta_grid, incumbent, integrator="qk21", shard=0,
+                    n_shards=1):
     """Full-tree MPC step (run_math_model.py:133-228): S1^3 leaves from the
     device grids v_grid [|V|], beta_grid [|B|] (fp64 tensors on the engine's
-    device).  Returns the device result buffer (uint8[FT_RESULT_BYTES])."""
+    device); this call evaluates leaf shard `shard` of `n_shards`.  Returns
+    the device result buffer (uint8[FT_RESULT_BYTES])."""
     from .abi import FT_RESULT_BYTES
     lib = engine.lib
     nv, nb = v_grid.numel(), beta_grid.numel()
@@ -172,8 +174,8 @@ def fulltree_argmin(engine, problem, v_grid, beta_grid, incumbent, integrator="q
     out = torch.empty(FT_RESULT_BYTES, dtype=torch.uint8, device=engine.device)
     st = lib.mpc_fulltree_argmin(ctypes.byref(problem), v_grid.data_ptr(), nv,
                                  beta_grid.data_ptr(), nb, float(incumbent),
-                                 _integ(integrator), ws.data_ptr(), ws.numel(), out.data_ptr(),
-                                 _stream_ptr())
+                                 _integ(integrator), int(shard), int(n_shards), ws.data_ptr(),
+                                 ws.numel(), out.data_ptr(), _stream_ptr())
     native.check(st, "mpc_fulltree_argmin")
     return out
 

@@ -126,7 +126,8 @@ def lib():
     L.mpc_fulltree_workspace_bytes.argtypes = [_I32, _I32]
     L.mpc_fulltree_argmin.restype = ctypes.c_int
     L.mpc_fulltree_argmin.argtypes = [ctypes.POINTER(MpcFulltreeProblem), _P, _I32, _P, _I32,
-                                      ctypes.c_double, _I32, _P, ctypes.c_size_t, _P, _P]
+                                      ctypes.c_double, _I32, _I32, _I32, _P, ctypes.c_size_t,
+                                      _P, _P]
     L.mpc_episode_rollout.restype = ctypes.c_int
     L.mpc_episode_rollout.argtypes = [_P, _P, _P, _I64, _I32, _I64, _I32, _P, ctypes.c_size_t,
                                       _P, ctypes.POINTER(MpcEpisodeConfig), _P, _I32, _P]

@@ -54,6 +54,16 @@ optimal_criterion = None
 
 _engine = None
 _grids_dev = None
+_group = None            # torch.distributed group when the leaves are sharded over ranks
+
+
+def shard_over(group=None):
+    """Shard every predictive_control's leaves over the ranks of `group`
+    (torch.distributed, one process per GPU): each rank evaluates a contiguous
+    leaf range, one all_gather of the 200-B results selects the winner on
+    every rank.  shard_over(None) returns to single-device evaluation."""
+    global _group
+    _group = group
 
 
 def configure(delta_v=_cfg.delta_v, delta_beta=_cfg.delta_beta):
@@ -127,7 +137,15 @@ def predictive_control(_initial_x, _initial_y, _initial_phi, _initial_velocity, 
                            float(x_t), float(y_t), float(x_0), float(y_0),
                            float(np.arctan(x_t / y_t)), float(L), float(t),
                            float(t + delta_t))
-    r = fulltree_result(fulltree_argmin(eng, p, vg, bg, optimal_criterion, INTEGRATOR))
+    if _group is None:
+        r = fulltree_result(fulltree_argmin(eng, p, vg, bg, optimal_criterion, INTEGRATOR))
+    else:
+        import torch.distributed as dist
+        from .distributed import gather_bytes, select_fulltree
+        rank, world = dist.get_rank(_group), dist.get_world_size(_group)
+        local = fulltree_argmin(eng, p, vg, bg, optimal_criterion, INTEGRATOR, rank, world)
+        gathered = gather_bytes(local, _group)
+        r = select_fulltree(gathered.cpu().numpy().tobytes(), optimal_criterion)
     if r.found:
         optimal_criterion = r.cost
         optimal_trajectory = [[r.trajectory()[i] + ([r.v[0], r.beta[0]] if i == 0 else [])
@@ -181,6 +199,6 @@ def run_episode(seed=None, max_calls=None):
     return records, "on_target"
 
 
-__all__ = ["configure", "is_on_target", "get_distance_from_line", "get_distance_from_target",
+__all__ = ["configure", "shard_over", "is_on_target", "get_distance_from_line", "get_distance_from_target",
            "saturation", "control_criterion", "predictive_control", "start_episode",
            "run_episode", "prediction_horizon"]

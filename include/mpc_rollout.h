@@ -245,11 +245,15 @@ typedef struct mpc_fulltree_result {
 } mpc_fulltree_result_t;
 
 size_t mpc_fulltree_workspace_bytes(int32_t n_v, int32_t n_beta);
-/* v_grid / beta_grid: device arrays; out: device pointer. */
+/* v_grid / beta_grid: device arrays; out: device pointer.  shard / n_shards:
+ * this call evaluates the shard-th of n_shards contiguous parts of the leaf
+ * set (leaf indices stay global); the winner over all shards is the
+ * lexicographic (cost, leaf) minimum of the shards' results (multi-GPU:
+ * one all_gather of the results per MPC step). */
 int mpc_fulltree_argmin(const mpc_fulltree_problem_t* p, const double* v_grid, int32_t n_v,
                         const double* beta_grid, int32_t n_beta, double incumbent,
-                        int32_t integrator, void* ws, size_t ws_bytes,
-                        mpc_fulltree_result_t* out, mpc_stream_t stream);
+                        int32_t integrator, int32_t shard, int32_t n_shards, void* ws,
+                        size_t ws_bytes, mpc_fulltree_result_t* out, mpc_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -109,3 +109,58 @@ def test_select_winner_host_order():
     assert select_winner_host(recs, incumbent=5.0).found == 0      # strict <
     none = select_winner_host([rec(float("inf"), -1)] * 2)
     assert (none.index, none.found) == (-1, 0)
+
+
+def _ft_worker(rank, world, port, q):
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from diplomjourney_amd.abi import FT_RESULT_BYTES, MpcFulltreeResult
+        from diplomjourney_amd.distributed import gather_bytes, select_fulltree, shard_range
+        from oracle import oracle as O
+        V, B = [0.0, 0.5, 1.0], [-0.5, 0.0, 0.5]
+        r = O.fulltree_argmin(V, B, (0.2, -0.1, 0.4), (3.0, 4.0), (0.0, 0.0),
+                              float(np.arctan(3.0 / 4.0)), 0.5, 0.05, 0.1, 1e18, detail=True)
+        costs = r["costs"]
+        lo, hi = shard_range(len(costs), rank, world)
+        k = lo + int(np.argmin(costs[lo:hi]))
+        res = MpcFulltreeResult()
+        res.cost, res.leaf, res.s1 = float(costs[k]), k, 9
+        local = torch.frombuffer(bytearray(bytes(res)), dtype=torch.uint8)
+        assert local.numel() == FT_RESULT_BYTES
+        win = select_fulltree(gather_bytes(local).numpy().tobytes(), incumbent=1e18)
+        q.put((rank, win.leaf, win.cost, win.found, r["leaf"], r["cost"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_fulltree_shards_match_single_scan():
+    """Full tree (run_math_model.py): per-rank leaf shards + one all_gather of
+    the result records + lexicographic selection == the single scan."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ft_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, leaf, cost, found, ref_leaf, ref_cost in outs:
+        assert (leaf, cost, found) == (ref_leaf, ref_cost, 1)
+
+
+def test_select_fulltree_order():
+    from diplomjourney_amd.abi import MpcFulltreeResult
+    from diplomjourney_amd.distributed import select_fulltree
+
+    def rec(cost, leaf):
+        r = MpcFulltreeResult()
+        r.cost, r.leaf = cost, leaf
+        return r
+    recs = [rec(2.0, 900), rec(2.0, 40), rec(float("inf"), -1), rec(3.0, 0)]
+    w = select_fulltree(recs, incumbent=5.0)
+    assert (w.leaf, w.found) == (40, 1)
+    assert select_fulltree(recs, incumbent=2.0).found == 0          # strict <

@@ -105,3 +105,24 @@ def test_drop_in_episodes(engine, gold):
                                     rel_tol=COST_RTOL)
     finally:
         rmm.configure()
+
+
+@pytest.mark.parametrize("n_shards", [2, 3, 8])
+def test_sharded_equals_single_launch(engine, n_shards):
+    """Leaf shards (the multi-GPU decomposition) evaluated one after another on
+    one GPU + the host selection == one launch, bit for bit."""
+    from diplomjourney_amd.abi import MpcFulltreeProblem
+    from diplomjourney_amd.distributed import select_fulltree
+    from diplomjourney_amd.expansion import fulltree_argmin, fulltree_result
+    V = np.round(np.arange(0.0, 1.0 + 0.1, 0.1), 3)
+    B = np.round(np.linspace(-1.047, 1.047, 21), 3)
+    vg = torch.tensor(V, dtype=torch.float64, device=engine.device)
+    bg = torch.tensor(B, dtype=torch.float64, device=engine.device)
+    p = MpcFulltreeProblem(0.3, -0.2, 0.5, 4.0, 5.0, 0.0, 0.0, float(np.arctan(0.8)), 0.5,
+                           0.1, 0.15)
+    one = fulltree_result(fulltree_argmin(engine, p, vg, bg, 1e18, "rect+rot"))
+    parts = [fulltree_result(fulltree_argmin(engine, p, vg, bg, 1e18, "rect+rot", s, n_shards))
+             for s in range(n_shards)]
+    win = select_fulltree(parts, 1e18)
+    assert (win.leaf, win.cost, win.found) == (one.leaf, one.cost, one.found)
+    assert win.trajectory() == one.trajectory()
