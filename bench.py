@@ -471,9 +471,12 @@ def bench_fulltree(args, wl, eng, rank, world, cpu):
     leaves = s1 ** 3
     rmm.start_episode(-3.0, -2.0, 0.3, 4.0, 5.0)
 
+    trace = []
+
     def step():
         c = rmm.predictive_control(rmm.x, rmm.y, rmm.phi, rmm.v, rmm.x_t, rmm.y_t)
         rmm.x, rmm.y, rmm.phi, rmm.v, rmm.beta = c
+        trace.append([float(z) for z in c] + [float(rmm.optimal_criterion)])
 
     for _ in range(args.warmup):
         step()
@@ -495,6 +498,9 @@ def bench_fulltree(args, wl, eng, rank, world, cpu):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     per_step = elapsed / args.steps
+    if args.dump_log and rank == 0:
+        with open(args.dump_log, "w") as fh:
+            json.dump(trace, fh)
     flops = FT_FLOPS_PER_LEAF[args.integrator] * leaves / per_step / world   # per GPU
     out = {
         "metric": METRIC, "value": leaves * args.steps / elapsed, "unit": "leaves/s",
