@@ -197,4 +197,97 @@ __global__ __launch_bounds__(kFinBlock) void k_ft_finalize(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Robot-batched full tree (the run_math_model.py:231-280 episodes run side by
+// side, one robot per episode, in lockstep: every robot's MPC step k uses the
+// same quad window, so the per-control table is shared).  blockIdx.y = robot.
+
+struct FtRobot {
+  Consts K;
+  double atan_t;
+};
+
+__global__ void k_ft_robots(const mpc_fulltree_problem_t* __restrict__ probs, int n,
+                            double L, double t_a, double t_b, FtRobot* __restrict__ robots) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  mpc_problem_t q;
+  q.x = probs[r].x;
+  q.y = probs[r].y;
+  q.phi = probs[r].phi;
+  q.x_t = probs[r].x_t;
+  q.y_t = probs[r].y_t;
+  q.x_0 = probs[r].x_0;
+  q.y_0 = probs[r].y_0;
+  q.L = L;
+  q.t_a = t_a;
+  q.t_b = t_b;
+  robots[r].K = consts_from_problem(q);
+  robots[r].atan_t = probs[r].atan_target;
+}
+
+template <int INTEG, bool ROT>
+__global__ __launch_bounds__(kBlock) void k_ft_leaves_batched(
+    const FtRobot* __restrict__ robots, const FtCtl* __restrict__ ctl,
+    const uint32_t* __restrict__ no_rot, int64_t s1, Rec* __restrict__ part) {
+  const int r = blockIdx.y;
+  const Consts K = robots[r].K;
+  const double atan_t = robots[r].atan_t;
+  const int64_t n_items = ((s1 * s1 + 63) / 64) * ((s1 + kFtChunk - 1) / kFtChunk);
+  uint64_t best_k = ~0ull;
+  int64_t best_i = INT64_MAX;
+  if (ROT && *no_rot == 0u)
+    ft_leaves_body<INTEG, true>(K, atan_t, ctl, s1, 0, n_items, best_k, best_i);
+  else
+    ft_leaves_body<INTEG, false>(K, atan_t, ctl, s1, 0, n_items, best_k, best_i);
+  block_argmin(best_k, best_i);
+  if (threadIdx.x == 0) part[static_cast<int64_t>(r) * gridDim.x + blockIdx.x] =
+      Rec{best_k, best_i};
+}
+
+template <int INTEG, bool ROT>
+__global__ __launch_bounds__(kBlock) void k_ft_finalize_batched(
+    const Rec* __restrict__ part, int n_part, const FtRobot* __restrict__ robots,
+    const FtCtl* __restrict__ ctl, const uint32_t* __restrict__ no_rot, int64_t s1,
+    const double* __restrict__ incumbents, mpc_fulltree_result_t* __restrict__ outs) {
+  const int r = blockIdx.x;
+  uint64_t k = ~0ull;
+  int64_t i = INT64_MAX;
+  for (int p = threadIdx.x; p < n_part; p += kBlock) {
+    const Rec rec = part[static_cast<int64_t>(r) * n_part + p];
+    if (rec_less(rec.key, rec.idx, k, i)) {
+      k = rec.key;
+      i = rec.idx;
+    }
+  }
+  block_argmin(k, i);
+  if (threadIdx.x != 0) return;
+  mpc_fulltree_result_t* out = outs + r;
+  const Consts& K = robots[r].K;
+  out->s1 = static_cast<int32_t>(s1);
+  if (k == ~0ull) {
+    out->cost = __builtin_inf();
+    out->leaf = -1;
+    out->found = 0;
+    return;
+  }
+  const double c = key_cost(k);
+  out->cost = c;
+  out->leaf = i;
+  out->found = c < (incumbents ? incumbents[r] : __builtin_inf()) ? 1 : 0;
+  const int64_t kk[3] = {i / (s1 * s1), (i / s1) % s1, i % s1};
+  const bool rot = ROT && *no_rot == 0u;
+  FtState st{K.x, K.y, K.phi, K.s0, K.c0};
+  for (int l = 0; l < 3; ++l) {
+    const FtCtl u = ctl[kk[l]];
+    st = rot ? ft_apply<INTEG, true>(st, u, K) : ft_apply<INTEG, false>(st, u, K);
+    out->k[l] = kk[l];
+    out->v[l] = u.v;
+    out->beta[l] = u.beta;
+    out->traj[l][0] = st.x;
+    out->traj[l][1] = st.y;
+    out->traj[l][2] = st.ph;
+  }
+}
+
 }  // namespace mpc

@@ -504,4 +504,62 @@ int mpc_fulltree_argmin(const mpc_fulltree_problem_t* p, const double* v_grid, i
   return last_hip_status();
 }
 
+static int64_t ft_blocks_per_robot(int64_t s1, int32_t n) {
+  const int64_t n_items = cdiv(s1 * s1, 64) * cdiv(s1, kFtChunk);
+  // about 4096 blocks in total, at least one per robot
+  const int64_t want = std::max<int64_t>(1, 4096 / std::max<int32_t>(n, 1));
+  return std::max<int64_t>(1, std::min(cdiv(n_items, kWaves), want));
+}
+
+size_t mpc_fulltree_batched_workspace_bytes(int32_t n_problems, int32_t n_v, int32_t n_beta) {
+  if (n_problems < 1 || n_v < 1 || n_beta < 1) return 0;
+  const int64_t s1 = static_cast<int64_t>(n_v) * n_beta;
+  return ft_align(s1 * sizeof(FtCtl)) + 256 + ft_align(n_problems * sizeof(FtRobot)) +
+         static_cast<size_t>(n_problems) * ft_blocks_per_robot(s1, n_problems) * sizeof(Rec);
+}
+
+int mpc_fulltree_argmin_batched(const mpc_fulltree_problem_t* problems,
+                                const double* incumbents, int32_t n_problems, double L,
+                                double t_a, double t_b, const double* v_grid, int32_t n_v,
+                                const double* beta_grid, int32_t n_beta, int32_t integrator,
+                                void* ws, size_t ws_bytes, mpc_fulltree_result_t* out,
+                                mpc_stream_t stream) {
+  if (!problems || !out || !v_grid || !beta_grid || n_problems < 1 || n_v < 1 || n_beta < 1 ||
+      n_problems > 65535)
+    return MPC_ERR_ARG;
+  const int64_t s1 = static_cast<int64_t>(n_v) * n_beta;
+  if (s1 > 2000000) return MPC_ERR_ARG;
+  if (mode_ok(integrator) != MPC_OK) return MPC_ERR_UNSUPPORTED;
+  if (!ws || ws_bytes < mpc_fulltree_batched_workspace_bytes(n_problems, n_v, n_beta))
+    return MPC_ERR_WORKSPACE;
+  mpc_problem_t q = {};
+  q.x_t = 1.0;   // window-only constants for the shared control table
+  q.y_t = 1.0;
+  q.L = L;
+  q.t_a = t_a;
+  q.t_b = t_b;
+  const Consts Kw = host_consts(q);
+  char* w = static_cast<char*>(ws);
+  FtCtl* ctl = reinterpret_cast<FtCtl*>(w);
+  uint32_t* no_rot = reinterpret_cast<uint32_t*>(w + ft_align(s1 * sizeof(FtCtl)));
+  FtRobot* robots = reinterpret_cast<FtRobot*>(w + ft_align(s1 * sizeof(FtCtl)) + 256);
+  Rec* part = reinterpret_cast<Rec*>(w + ft_align(s1 * sizeof(FtCtl)) + 256 +
+                                     ft_align(n_problems * sizeof(FtRobot)));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(no_rot, 0, sizeof(uint32_t), st) != hipSuccess) return MPC_ERR_HIP;
+  const int64_t bx = ft_blocks_per_robot(s1, n_problems);
+  k_ft_robots<<<cdiv(n_problems, 256), 256, 0, st>>>(problems, n_problems, L, t_a, t_b, robots);
+  dispatch_mode(integrator, [&](auto integ, auto rot) {
+    constexpr int I = decltype(integ)::value;
+    constexpr bool R = decltype(rot)::value;
+    k_ft_controls<I><<<cdiv(s1, kBlock), kBlock, 0, st>>>(Kw, v_grid, beta_grid, n_beta, s1,
+                                                          ctl, no_rot);
+    k_ft_leaves_batched<I, R><<<dim3(static_cast<unsigned>(bx), n_problems), kBlock, 0, st>>>(
+        robots, ctl, no_rot, s1, part);
+    k_ft_finalize_batched<I, R><<<n_problems, kBlock, 0, st>>>(
+        part, static_cast<int>(bx), robots, ctl, no_rot, s1, incumbents, out);
+  });
+  return last_hip_status();
+}
+
 }  // extern "C"

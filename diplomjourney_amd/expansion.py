@@ -180,6 +180,33 @@ def fulltree_argmin(engine, problem, v_grid, beta_grid, incumbent, integrator="q
     return out
 
 
+def fulltree_argmin_batched(engine, problems_dev, incumbents_dev, L, t_a, t_b, v_grid,
+                            beta_grid, integrator="qk21", out=None):
+    """R robots' full trees (one per run_math_model episode, lockstep):
+    problems_dev uint8[R * sizeof(mpc_fulltree_problem_t)], incumbents_dev
+    float64[R]; returns the device results uint8[R * FT_RESULT_BYTES]."""
+    from .abi import FT_RESULT_BYTES, MpcFulltreeProblem
+    lib = engine.lib
+    R = problems_dev.numel() // ctypes.sizeof(MpcFulltreeProblem)
+    nv, nb = v_grid.numel(), beta_grid.numel()
+    ws = engine._workspace(lib.mpc_fulltree_batched_workspace_bytes(R, nv, nb))
+    if out is None:
+        out = torch.empty(R * FT_RESULT_BYTES, dtype=torch.uint8, device=engine.device)
+    st = lib.mpc_fulltree_argmin_batched(
+        problems_dev.data_ptr(), incumbents_dev.data_ptr(), R, float(L), float(t_a),
+        float(t_b), v_grid.data_ptr(), nv, beta_grid.data_ptr(), nb, _integ(integrator),
+        ws.data_ptr(), ws.numel(), out.data_ptr(), _stream_ptr())
+    native.check(st, "mpc_fulltree_argmin_batched")
+    return out
+
+
+def fulltree_results(out_dev):
+    from .abi import FT_RESULT_BYTES, MpcFulltreeResult
+    raw = out_dev.cpu().numpy().tobytes()
+    return [MpcFulltreeResult.from_buffer_copy(raw[i:i + FT_RESULT_BYTES])
+            for i in range(0, len(raw), FT_RESULT_BYTES)]
+
+
 def fulltree_result(out_dev):
     from .abi import MpcFulltreeResult
     return MpcFulltreeResult.from_buffer_copy(out_dev.cpu().numpy().tobytes())

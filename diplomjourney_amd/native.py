@@ -32,6 +32,7 @@ EXPORTS = (
     "mpc_episode_expand", "mpc_episode_advance", "mpc_episode_sample", "mpc_episode_partials",
     "mpc_episode_finalize", "mpc_episode_rollout",
     "mpc_fulltree_workspace_bytes", "mpc_fulltree_argmin",
+    "mpc_fulltree_batched_workspace_bytes", "mpc_fulltree_argmin_batched",
 )
 
 HIPCC_FLAGS = [
@@ -128,6 +129,12 @@ def lib():
     L.mpc_fulltree_argmin.argtypes = [ctypes.POINTER(MpcFulltreeProblem), _P, _I32, _P, _I32,
                                       ctypes.c_double, _I32, _I32, _I32, _P, ctypes.c_size_t,
                                       _P, _P]
+    L.mpc_fulltree_batched_workspace_bytes.restype = ctypes.c_size_t
+    L.mpc_fulltree_batched_workspace_bytes.argtypes = [_I32, _I32, _I32]
+    L.mpc_fulltree_argmin_batched.restype = ctypes.c_int
+    L.mpc_fulltree_argmin_batched.argtypes = [_P, _P, _I32, ctypes.c_double, ctypes.c_double,
+                                              ctypes.c_double, _P, _I32, _P, _I32, _I32, _P,
+                                              ctypes.c_size_t, _P, _P]
     L.mpc_episode_rollout.restype = ctypes.c_int
     L.mpc_episode_rollout.argtypes = [_P, _P, _P, _I64, _I32, _I64, _I32, _P, ctypes.c_size_t,
                                       _P, ctypes.POINTER(MpcEpisodeConfig), _P, _I32, _P]

@@ -26,7 +26,8 @@ import torch
 
 from . import config as _cfg
 from .abi import MpcFulltreeProblem
-from .expansion import Expansion, fulltree_argmin, fulltree_result
+from .expansion import (Expansion, fulltree_argmin, fulltree_argmin_batched, fulltree_result,
+                        fulltree_results)
 
 L = _cfg.L
 delta_t = _cfg.delta_t
@@ -199,6 +200,101 @@ def run_episode(seed=None, max_calls=None):
     return records, "on_target"
 
 
-__all__ = ["configure", "shard_over", "is_on_target", "get_distance_from_line", "get_distance_from_target",
+def draw_starts(n, seed=None):
+    """Start and target of n consecutive episodes exactly as the script's loop
+    draws them (:235-239, five numpy uniforms per episode, one RNG stream)."""
+    if seed is not None:
+        np.random.seed(seed)
+    out = []
+    for _ in range(n):
+        x0 = np.random.uniform(-10, 10)
+        y0 = np.random.uniform(-10, 10)
+        phi0 = np.random.uniform(-math.pi, math.pi)
+        xt = np.random.uniform(x0 - 10, x0 + 10)
+        yt = np.random.uniform(y0 - 10, y0 + 10)
+        out.append((x0, y0, phi0, xt, yt))
+    return out
+
+
+class _Robot:
+    """One episode's state (the script's module globals, per robot)."""
+
+    def __init__(self, start):
+        self.x_0, self.y_0, self.phi_0, self.x_t, self.y_t = start
+        self.x, self.y, self.phi, self.v, self.beta = self.x_0, self.y_0, self.phi_0, 0, 0
+        self.t = 0
+        self.atan_t = float(np.arctan(self.x_t / self.y_t))
+        self.crit = self._criterion0()
+        self.stale = None            # optimal_trajectory[0][0] of the last winner
+        self.k = 0
+        self.prev = (self.x, self.y)
+        self.records = []
+        self.stop = None
+
+    def _criterion0(self):
+        # control_criterion([x_0, y_0, phi_0]) with this episode's globals (:82-86)
+        angle = (np.arctan(self.x_t / self.y_t) - self.phi_0)
+        dist_t = math.sqrt((self.x_t - self.x_0) ** 2 + (self.y_t - self.y_0) ** 2)
+        return 10000 * dist_t + 10 * angle ** 2 + 100 * 1000 ** 2
+
+
+def run_batched(starts, max_calls=None, integrator=None):
+    """The script's episode loop (:231-280) for len(starts) episodes at once:
+    one robot per episode, all robots step in lockstep, and every MPC step of
+    all still-running episodes is ONE batched full-tree launch
+    (mpc_fulltree_argmin_batched).  Each robot keeps its own never-reset
+    incumbent, stale winner and stop rule.  Returns [(records, stop)] per
+    episode, as run_episode does."""
+    eng, (vg, bg) = _device()
+    integ = INTEGRATOR if integrator is None else integrator
+    robots = [_Robot(s) for s in starts]
+    step = 0
+    while True:
+        live = []
+        for r in robots:
+            if r.stop is not None:
+                continue
+            if is_on_target_of(r):
+                r.stop = "on_target"
+            elif max_calls is not None and len(r.records) == max_calls:
+                r.stop = "max_calls"
+            else:
+                live.append(r)
+        if not live:
+            break
+        t_now = live[0].t + delta_t                       # lockstep: one window (:156)
+        probs = (MpcFulltreeProblem * len(live))(*[
+            MpcFulltreeProblem(float(r.x), float(r.y), float(r.phi), float(r.x_t),
+                               float(r.y_t), float(r.x_0), float(r.y_0), r.atan_t, float(L),
+                               t_now, t_now + delta_t) for r in live])
+        pd = torch.frombuffer(bytearray(bytes(probs)), dtype=torch.uint8).to(eng.device)
+        inc = torch.tensor([r.crit for r in live], dtype=torch.float64, device=eng.device)
+        res = fulltree_results(fulltree_argmin_batched(eng, pd, inc, L, t_now, t_now + delta_t,
+                                                       vg, bg, integ))
+        for r, w in zip(live, res):
+            pre = (r.x, r.y, r.phi, r.v, r.t, r.crit)
+            r.t = t_now
+            if w.found:
+                r.crit = w.cost
+                r.stale = [w.traj[0][0], w.traj[0][1], w.traj[0][2], w.v[0], w.beta[0]]
+            if r.stale is None:
+                raise TypeError("'int' object is not subscriptable")   # as the script
+            coords = list(r.stale)
+            r.records.append({"pre": pre, "ret": coords, "optimal_criterion": r.crit})
+            r.x, r.y, r.phi, r.v, r.beta = coords
+            if r.x == r.prev[0] and r.y == r.prev[1]:
+                r.k += 1
+            if r.k == 2:
+                r.stop = "recursive_error"
+            r.prev = (r.x, r.y)
+        step += 1
+    return [(r.records, r.stop) for r in robots]
+
+
+def is_on_target_of(r):
+    return (r.x_t - r.x) ** 2 + (r.y_t - r.y) ** 2 <= eps
+
+
+__all__ = ["configure", "shard_over", "draw_starts", "run_batched", "is_on_target", "get_distance_from_line", "get_distance_from_target",
            "saturation", "control_criterion", "predictive_control", "start_episode",
            "run_episode", "prediction_horizon"]

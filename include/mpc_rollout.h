@@ -255,6 +255,20 @@ int mpc_fulltree_argmin(const mpc_fulltree_problem_t* p, const double* v_grid, i
                         int32_t integrator, int32_t shard, int32_t n_shards, void* ws,
                         size_t ws_bytes, mpc_fulltree_result_t* out, mpc_stream_t stream);
 
+/* R robots' full trees in one launch sequence (the run_math_model.py:231-280
+ * episodes side by side, one robot per episode, stepping in lockstep).
+ * problems / incumbents / out: device arrays [n_problems]; the problems' L,
+ * t_a, t_b are ignored: every robot uses (L, t_a, t_b) given here (lockstep
+ * robots share the MPC step's quad window).  Problem constants are derived
+ * on the device (squares as x*x). */
+size_t mpc_fulltree_batched_workspace_bytes(int32_t n_problems, int32_t n_v, int32_t n_beta);
+int mpc_fulltree_argmin_batched(const mpc_fulltree_problem_t* problems,
+                                const double* incumbents, int32_t n_problems, double L,
+                                double t_a, double t_b, const double* v_grid, int32_t n_v,
+                                const double* beta_grid, int32_t n_beta, int32_t integrator,
+                                void* ws, size_t ws_bytes, mpc_fulltree_result_t* out,
+                                mpc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

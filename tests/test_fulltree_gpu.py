@@ -126,3 +126,47 @@ def test_sharded_equals_single_launch(engine, n_shards):
     win = select_fulltree(parts, 1e18)
     assert (win.leaf, win.cost, win.found) == (one.leaf, one.cost, one.found)
     assert win.trajectory() == one.trajectory()
+
+
+def test_batched_episodes_match_reference(engine, gold):
+    """The lockstep batched driver (one robot per episode, one batched
+    full-tree launch per MPC step) reproduces the three reference episodes."""
+    from diplomjourney_amd import run_math_model as rmm
+    cfg = gold["config"]
+    rmm.configure(cfg["delta_v"], cfg["delta_beta"])
+    try:
+        starts = [(e["x_0"], e["y_0"], e["phi_0"], e["x_t"], e["y_t"]) for e in gold["episodes"]]
+        outs = rmm.run_batched(starts, max_calls=6)
+        for (recs, stop), ep in zip(outs, gold["episodes"]):
+            assert stop == ep["stop"] and len(recs) == len(ep["calls"])
+            assert recs[0]["pre"][5] == ep["first_incumbent"]
+            for r, c in zip(recs, ep["calls"]):
+                assert r["ret"][3:] == c["ret"][3:]
+                assert max(abs(a - b) for a, b in zip(r["ret"][:3], c["ret"][:3])) <= STATE_TOL
+                assert math.isclose(r["optimal_criterion"], c["post"]["optimal_criterion"],
+                                    rel_tol=COST_RTOL)
+    finally:
+        rmm.configure()
+
+
+def test_batched_equals_sequential_episodes(engine):
+    """24 random episodes (the script's RNG stream) at S1 = 35: batched
+    lockstep driver == one episode after another through predictive_control."""
+    from diplomjourney_amd import run_math_model as rmm
+    rmm.configure(0.25, math.radians(20))
+    try:
+        starts = rmm.draw_starts(24, seed=11)
+        batched = rmm.run_batched(starts, max_calls=5)
+        for s, (recs, stop) in zip(starts, batched):
+            rmm.start_episode(*s)
+            seq = []
+            for _ in range(len(recs)):
+                c = rmm.predictive_control(rmm.x, rmm.y, rmm.phi, rmm.v, rmm.x_t, rmm.y_t)
+                seq.append((c, rmm.optimal_criterion))
+                rmm.x, rmm.y, rmm.phi, rmm.v, rmm.beta = c
+            for r, (c, crit) in zip(recs, seq):
+                assert r["ret"][3:] == c[3:]
+                assert max(abs(a - b) for a, b in zip(r["ret"][:3], c[:3])) <= STATE_TOL
+                assert math.isclose(r["optimal_criterion"], crit, rel_tol=COST_RTOL)
+    finally:
+        rmm.configure()
