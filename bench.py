@@ -62,6 +62,10 @@ WORKLOADS = {
                    "S1^3 = 9.17e7 leaves per MPC step, heading-term criterion, never-reset "
                    "incumbent; episode of the run_math_model drop-in"),
 }
+WORKLOADS["G"] = dict(n_steps=3, per_gpu=None, robots=1000,
+                      desc="run_math_model.py's 1000 episodes (SURVEY 8f 4): one robot per "
+                           "episode, lockstep, one batched full-tree launch per MPC step, "
+                           "S1 = 5 x 13 controls (274,625 leaves per robot-step)")
 FP64_VECTOR_PEAK_TFLOPS = 78.6   # MI355X spec (2 x 32 lanes x 2 flops/clk/SIMD at 2.4 GHz / 2)
 # fp64 operations per full-tree leaf (csrc/mpc_fulltree.h, one layer step + criterion), as
 # written: rect+rot 34 (heading add 1, rotation 8, two fused position updates 4, criterion 21);
@@ -152,7 +156,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = (cpu_baseline_fulltree(args.cpu_seconds) if args.workload == "F"
+        cpu = (cpu_baseline_fulltree(args.cpu_seconds) if args.workload in ("F", "G")
                else cpu_baseline(wl, args.cpu_seconds))
 
     import torch
@@ -173,6 +177,8 @@ def main():
         return bench_robots(args, wl, eng, rank, world, cpu)
     if args.workload == "F":
         return bench_fulltree(args, wl, eng, rank, world, cpu)
+    if args.workload == "G":
+        return bench_episodes(args, wl, eng, rank, world, cpu)
 
     from diplomjourney_amd.episode import DeviceEpisode, Episode, percentile
     n_total = (args.candidates_per_gpu or wl["per_gpu"]) * world
@@ -519,6 +525,59 @@ def bench_fulltree(args, wl, eng, rank, world, cpu):
                      "note": "algorithmic fp64 ops per leaf as written (FT_FLOPS_PER_LEAF); "
                              "leaves are generated from the index, no HBM stream"},
         "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_episodes(args, wl, eng, rank, world, cpu):
+    """Config G: the script's episode loop for 1000 episodes at once (robots
+    sharded over ranks, no exchange).  A timed step = one batched full-tree
+    launch over every still-running robot + the host episode updates; K steps
+    of run_batched (episodes stopped by --steps as max_calls)."""
+    import math as _m
+    import torch
+    import torch.distributed as dist
+    from diplomjourney_amd import run_math_model as rmm
+    from diplomjourney_amd.distributed import shard_range
+    rmm.INTEGRATOR = args.integrator
+    rmm.configure(0.25, _m.radians(10))
+    s1 = int(rmm.size_max_1)
+    starts = rmm.draw_starts(wl["robots"], seed=20261015)
+    lo, hi = shard_range(len(starts), rank, world)
+    rmm.run_batched(starts[lo:hi], max_calls=max(1, args.warmup))      # warmup
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    outs = rmm.run_batched(starts[lo:hi], max_calls=args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    robot_steps = sum(len(r) for r, _ in outs)
+    t = torch.tensor([elapsed, robot_steps], dtype=torch.float64, device=eng.device)
+    if world > 1:
+        mx = t[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed, robot_steps = float(mx.item()), float(t[1].item())
+    leaves = robot_steps * s1 ** 3
+    stops = {}
+    for _, st in outs:
+        stops[st] = stops.get(st, 0) + 1
+    out = {
+        "metric": METRIC, "value": leaves / elapsed, "unit": "leaves/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": wl["desc"], "s1": s1, "robots": wl["robots"],
+                   "robot_steps": robot_steps, "integrator": args.integrator,
+                   "episode_stops_rank0": stops,
+                   "parallelism": f"robot-sharded x{world}, no exchange"},
+        "roofline": None, "cpu_baseline": cpu,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
