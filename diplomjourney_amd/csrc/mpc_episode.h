@@ -191,6 +191,13 @@ __device__ inline void turn_target(double ax, double ay, double aphi, double d, 
   }
 }
 
+// r.tr[k][q] for a runtime k in {0, 1, 2} by selects: a dynamically indexed
+// local array would live in scratch memory (a ~µs round trip per access).
+__device__ __forceinline__ double tr_at(const Winner& r, int k, int q) {
+  const double a = r.tr[0][q], b = r.tr[1][q], c = r.tr[2][q];
+  return k == 0 ? a : (k == 1 ? b : c);
+}
+
 // Episode._advance: finishing logic (:392-414), events (:564-569), restart.
 // Operates on a register copy of the episode scalars (the caller loads it
 // once and stores it back once).
@@ -219,13 +226,13 @@ __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeHea
       k = 1;
       S->m += 1;
     } else {
-      const double ex = S->x_t - r.tr[probe][0], ey = S->y_t - r.tr[probe][1];
+      const double ex = S->x_t - tr_at(r, probe, 0), ey = S->y_t - tr_at(r, probe, 1);
       if (ex * ex + ey * ey <= c.eps) S->m += 1;
     }
     k = k < last ? k : last;
-    S->x = r.tr[k][0];
-    S->y = r.tr[k][1];
-    S->phi = r.tr[k][2];
+    S->x = tr_at(r, k, 0);
+    S->y = tr_at(r, k, 1);
+    S->phi = tr_at(r, k, 2);
     S->v = r.v;
     S->beta = r.beta;
     double tx, ty;

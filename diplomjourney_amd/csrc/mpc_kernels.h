@@ -434,38 +434,44 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
     w = K.L_pow2 ? vs * K.inv_L : vs / K.L;
     const double d = heading_incr<INTEG>(w, trig::tan_small(bs), K);
     s_dphi[lane] = d;
-    if (!(fabs(bs) <= trig::kTanMax) || (ROT && !(fabs(d) <= trig::kRotMax))) s_bad = 1;
+    const bool lane_bad =
+        !(fabs(bs) <= trig::kTanMax) || (ROT && !(fabs(d) <= trig::kRotMax));
+    if (lane_bad) s_bad = 1;
+    // rotation mode: the factors depend on this step's increment only, so
+    // they are formed here, in the same phase (no heading chain needed)
+    if (ROT && !lane_bad) trig::rotation_factors(d, s_a[lane], s_c[lane]);
   }
   __syncthreads();
-  if (valid && lane == 0) {
-    double ph = K.phi;
-    for (int st = 0; st < n_steps; ++st) {
-      ph = ph + s_dphi[st];
-      s_phi[st] = ph;
-      if (!ROT && !(fabs(ph) <= trig::kFastMax)) s_bad = 1;
-    }
-  }
-  __syncthreads();
-  if (s_bad) {
-    if (valid && lane < n_steps) s_dphi[lane] = heading_incr<INTEG>(w, trig::tan_fast(bs), K);
-    __syncthreads();
+  // Regular rotation-mode winner: ONE serial pass on lane 0 (heading, rotation,
+  // position); every other case keeps the heading chain / sincos phases.
+  const bool fast = ROT && s_bad == 0;
+  if (!fast) {
     if (valid && lane == 0) {
       double ph = K.phi;
       for (int st = 0; st < n_steps; ++st) {
         ph = ph + s_dphi[st];
         s_phi[st] = ph;
+        if (!ROT && !(fabs(ph) <= trig::kFastMax)) s_bad = 1;
       }
     }
     __syncthreads();
-  }
-  const bool bad = s_bad != 0;
-  if (valid && lane < n_steps) {
-    if (ROT && !bad)
-      trig::rotation_factors(s_dphi[lane], s_a[lane], s_c[lane]);
-    else
+    if (s_bad) {
+      if (valid && lane < n_steps)
+        s_dphi[lane] = heading_incr<INTEG>(w, trig::tan_fast(bs), K);
+      __syncthreads();
+      if (valid && lane == 0) {
+        double ph = K.phi;
+        for (int st = 0; st < n_steps; ++st) {
+          ph = ph + s_dphi[st];
+          s_phi[st] = ph;
+        }
+      }
+      __syncthreads();
+    }
+    if (valid && lane < n_steps)
       trig::sincos_fast(s_phi[lane], &s_a[lane], &s_c[lane]);  // == sincos_core if regular
+    __syncthreads();
   }
-  __syncthreads();
   if (lane != 0) return;
   out->n_steps = n_steps;
   if (win) win->n_steps = n_steps;
@@ -496,11 +502,13 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
     win->v = s_v[0];
     win->beta = s_b0;
   }
-  double x = K.x, y = K.y, sn = K.s0, cs = K.c0;
+  double x = K.x, y = K.y, sn = K.s0, cs = K.c0, ph = K.phi;
   for (int st = 0; st < n_steps; ++st) {
-    if (ROT && !bad) {
+    if (fast) {
+      ph = ph + s_dphi[st];
       trig::rotate_by(s_a[st], s_c[st], sn, cs);
     } else {
+      ph = s_phi[st];
       sn = s_a[st];
       cs = s_c[st];
     }
@@ -508,11 +516,11 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
     y = position_step<INTEG>(y, s_v[st], sn, K);
     out->traj[st][0] = x;
     out->traj[st][1] = y;
-    out->traj[st][2] = s_phi[st];
+    out->traj[st][2] = ph;
     if (win && st < 3) {
       win->tr[st][0] = x;
       win->tr[st][1] = y;
-      win->tr[st][2] = s_phi[st];
+      win->tr[st][2] = ph;
     }
   }
 }
@@ -571,6 +579,9 @@ __device__ __forceinline__ void finalize_block(
     const double* __restrict__ b, int64_t n_cand, int n_steps, int64_t index_base,
     double incumbent, mpc_result_t* __restrict__ out, const mpc_episode_config_t& ecfg,
     const EpisodeHook& hook) {
+#ifdef MPC_FIN_TRACE
+  const uint64_t tr0 = __builtin_amdgcn_s_memrealtime();
+#endif
   // One-GPU episode: thread 0 loads the episode scalars now, in parallel with
   // everything below, and stores them back once after the update.
   EpisodeHead H;
@@ -599,13 +610,21 @@ __device__ __forceinline__ void finalize_block(
         i = static_cast<int64_t>(r[q].y);
       }
   } else {
-    for (int p = threadIdx.x; p < n_part; p += NT) {
-      const Rec r = part[p];
-      if (rec_less(r.key, r.idx, k, i)) {
-        k = r.key;
-        i = r.idx;
-      }
+    // all of this thread's records are loaded before any is compared, so
+    // the loads overlap (one memory round trip)
+    constexpr int kPer = (kMaxBlocks + NT - 1) / NT;
+    Rec r[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int p = threadIdx.x + q * NT;
+      r[q] = p < n_part ? part[p] : Rec{~0ull, INT64_MAX};
     }
+#pragma unroll
+    for (int q = 0; q < kPer; ++q)
+      if (rec_less(r[q].key, r[q].idx, k, i)) {
+        k = r[q].key;
+        i = r[q].idx;
+      }
   }
   wave_argmin(k, i);
   if ((threadIdx.x & 63) == 0) {
@@ -620,12 +639,26 @@ __device__ __forceinline__ void finalize_block(
         i = s_idx[w];
       }
   }
+#ifdef MPC_FIN_TRACE
+  const uint64_t tr1 = __builtin_amdgcn_s_memrealtime();
+#endif
   Winner w;
   emit_winner<INTEG, ROT>(K, v, b, n_cand, n_steps, k, i, index_base + i, incumbent, out, &w);
+#ifdef MPC_FIN_TRACE
+  const uint64_t tr2 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (KDEV && hook.H && threadIdx.x == 0) {
     episode_hook(ecfg, hook, w, H);
     *hook.H = H;
   }
+#ifdef MPC_FIN_TRACE
+  if (threadIdx.x == 0) {   // debug builds only: 10-ns ticks in unused trajectory slots
+    const uint64_t tr3 = __builtin_amdgcn_s_memrealtime();
+    out->traj[31][0] = static_cast<double>(tr1 - tr0);
+    out->traj[31][1] = static_cast<double>(tr2 - tr1);
+    out->traj[31][2] = static_cast<double>(tr3 - tr2);
+  }
+#endif
 }
 
 template <int INTEG, bool ROT, bool KDEV>
