@@ -582,10 +582,13 @@ __device__ __forceinline__ void finalize_block(
 #ifdef MPC_FIN_TRACE
   const uint64_t tr0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  // One-GPU episode: thread 0 loads the episode scalars now, in parallel with
-  // everything below, and stores them back once after the update.
-  EpisodeHead H;
-  if (KDEV && hook.H && threadIdx.x == 0) H = *hook.H;
+  // One-GPU episode: the episode scalars are staged in LDS by wave 1 (one
+  // 8-B vector load per lane, issued after its record loads) and updated by
+  // thread 0 once the winner is known.  (Loading them into thread 0's SGPRs
+  // serialised three scalar round trips in front of wave 0's record loads.)
+  constexpr int kHeadWords = static_cast<int>(sizeof(EpisodeHead) / 8);
+  static_assert(sizeof(EpisodeHead) % 8 == 0 && kHeadWords <= 64 && NT >= 128, "head staging");
+  __shared__ uint64_t s_head[kHeadWords];
   __shared__ uint64_t s_key[NT / 64];
   __shared__ int64_t s_idx[NT / 64];
   uint64_t k = ~0ull;
@@ -626,6 +629,8 @@ __device__ __forceinline__ void finalize_block(
         i = r[q].idx;
       }
   }
+  if (KDEV && hook.H && threadIdx.x >= 64 && threadIdx.x < 64 + kHeadWords)
+    s_head[threadIdx.x - 64] = reinterpret_cast<const uint64_t*>(hook.H)[threadIdx.x - 64];
   wave_argmin(k, i);
   if ((threadIdx.x & 63) == 0) {
     s_key[threadIdx.x >> 6] = k;
@@ -647,7 +652,9 @@ __device__ __forceinline__ void finalize_block(
 #ifdef MPC_FIN_TRACE
   const uint64_t tr2 = __builtin_amdgcn_s_memrealtime();
 #endif
-  if (KDEV && hook.H && threadIdx.x == 0) {
+  if (KDEV && hook.H && threadIdx.x == 0) {   // emit_winner ended with a barrier
+    EpisodeHead H;
+    __builtin_memcpy(&H, s_head, sizeof(EpisodeHead));
     episode_hook(ecfg, hook, w, H);
     *hook.H = H;
   }
