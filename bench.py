@@ -76,8 +76,10 @@ FT_FLOPS_PER_LEAF = {"rect+rot": 34, "rect": 34, "qk21+rot": 78, "qk21": 78}
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 500 for the ~40 us expansion workloads, so the "
+                         "fixed graph-launch + sync cost (~0.2 ms) is amortised; 50 for F/G)")
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="C", choices=sorted(WORKLOADS))
     ap.add_argument("--integrator", default="rect+rot",
                     choices=["rect+rot", "rect", "qk21+rot", "qk21"],
@@ -105,7 +107,10 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r01_traffic.json"),
                     help="PMC-derived HBM bytes per launch for the roofline 'traffic' field "
                          "(tools/pmc.sh + tools/pmc_summary.py on the same kernel and config)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 50 if args.workload in ("F", "G") else 500
+    return args
 
 
 def cpu_baseline_fulltree(seconds):

@@ -193,6 +193,9 @@ __device__ __forceinline__ void rollout_lane_l(const Consts& K, const double* __
 // orders against the LDS reads: the waits are explicit (vmcnt for "slot
 // landed", lgkmcnt(0) before a slot is refilled) and every asm statement
 // clobbers memory.
+#ifndef MPC_GLDS_POLICY
+#define MPC_GLDS_POLICY " nt"   // control DMA is streamed once: non-temporal (A/B: -1.5 us/step on config C)
+#endif
 #ifndef MPC_RING
 #define MPC_RING 3           // LDS ring depth in steps (kRing-1 steps in flight)
 #endif
@@ -221,10 +224,10 @@ __device__ __forceinline__ void glds_pair(const double* gv, const double* gb, ui
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %3\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
+      "global_load_lds_dwordx4 %1, off" MPC_GLDS_POLICY "\n\t"
       "s_mov_b32 m0, %4\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %2, off\n\t"
+      "global_load_lds_dwordx4 %2, off" MPC_GLDS_POLICY "\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(gv), "v"(gb), "s"(dst_v), "s"(dst_b)
@@ -239,10 +242,10 @@ __device__ __forceinline__ void glds_refill(const double* gv, const double* gb, 
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %3\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
+      "global_load_lds_dwordx4 %1, off" MPC_GLDS_POLICY "\n\t"
       "s_mov_b32 m0, %4\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %2, off\n\t"
+      "global_load_lds_dwordx4 %2, off" MPC_GLDS_POLICY "\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(gv), "v"(gb), "s"(dst_v), "s"(dst_b), "v"(read_v.x), "v"(read_v.y),
