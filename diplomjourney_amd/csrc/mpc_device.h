@@ -96,24 +96,41 @@ MPC_HD __forceinline__ double position_step(double p, double v, double trig, con
 //                parameter, not a branch: a branch inside the step would split
 //                the loop into basic blocks and stop the scheduler from
 //                interleaving the lane's independent candidate chains.
+//   PL2 + RECT:  (v * inv_L) * h is formed as (v * h) * inv_L — the same
+//                value (scaling by a power of two commutes with rounding in the
+//                normal range) — so v * h is shared with the position update.
+//   ld:          VGPR-resident leading coefficients (trig::Leads), or nullptr.
 template <int INTEG, bool ROT, bool PL2>
 MPC_HD __forceinline__ void step_core(double& x, double& y, double& ph, double& s, double& c,
-                                      double v, double beta, const Consts& K, bool& bad) {
+                                      double v, double beta, const Consts& K, bool& bad,
+                                      const trig::Leads* ld = nullptr) {
   bad |= !(fabs(beta) <= trig::kTanMax);
-  const double w = PL2 ? v * K.inv_L : v / K.L;                // _velocity / L   (:78)
-  const double dphi = heading_incr<INTEG>(w, trig::tan_small(beta), K);  // angle_phi (:107)
+  const double t = trig::tan_small(beta, ld);
+  double dphi, vh = 0.0;
+  if constexpr (PL2 && INTEG == MPC_INTEG_RECT) {
+    vh = v * K.h;
+    dphi = (vh * K.inv_L) * t;                                 // angle_phi (:107)
+  } else {
+    const double w = PL2 ? v * K.inv_L : v / K.L;              // _velocity / L   (:78)
+    dphi = heading_incr<INTEG>(w, t, K);                       // angle_phi (:107)
+  }
   ph = ph + dphi;                                              // phi + _phi      (:113)
   if constexpr (ROT) {
     bad |= !(fabs(dphi) <= trig::kRotMax);
     double sd, cm1;
-    trig::rotation_factors(dphi, sd, cm1);
+    trig::rotation_factors(dphi, sd, cm1, ld);
     trig::rotate_by(sd, cm1, s, c);
   } else {
     bad |= !(fabs(ph) <= trig::kFastMax);
     trig::sincos_core(ph, &s, &c);
   }
-  x = position_step<INTEG>(x, v, c, K);                        // coordinate_x    (:99)
-  y = position_step<INTEG>(y, v, s, K);                        // coordinate_y    (:103)
+  if constexpr (PL2 && INTEG == MPC_INTEG_RECT) {
+    x = fma(vh, c, x);                                         // coordinate_x    (:99)
+    y = fma(vh, s, y);                                         // coordinate_y    (:103)
+  } else {
+    x = position_step<INTEG>(x, v, c, K);                      // coordinate_x    (:99)
+    y = position_step<INTEG>(y, v, s, K);                      // coordinate_y    (:103)
+  }
 }
 
 template <int INTEG>

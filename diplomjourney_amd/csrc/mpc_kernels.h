@@ -298,16 +298,21 @@ __device__ __forceinline__ void rollout_lane_glds(const Consts& K, const double*
   }
 #pragma unroll
   for (int u = 0; u < R - 1; ++u)
-    if (u < n_steps)
+    if (u < n_steps && MPC_EXPERIMENT != 2)
       glds_pair(v + u * ld + c0, b + u * ld + c0, dst(u), dst(u) + kSlot / 2);
   double2 v2 = make_double2(0.0, 0.0), b2 = v2;   // the last slot's contents as read
+  // leading trig coefficients pinned in VGPRs (opaque to the compiler, so not
+  // re-materialised per step)
+  trig::Leads lead = trig::const_leads();
+  asm volatile("" : "+v"(lead.tp), "+v"(lead.tq), "+v"(lead.rs), "+v"(lead.rc));
 #pragma unroll 1
   for (int s = 0; s < n_steps; s += R) {
 #pragma unroll
     for (int u = 0; u < R; ++u) {
       const int st = s + u;
       if (st < n_steps) {
-        if (st + R - 1 < n_steps) {
+        if (MPC_EXPERIMENT == 2) {
+        } else if (st + R - 1 < n_steps) {
           const int sr = st + R - 1, slot = (u + R - 1) % R;   // = the slot read last step
           glds_refill(v + sr * ld + c0, b + sr * ld + c0, dst(slot), dst(slot) + kSlot / 2, v2,
                       b2);
@@ -317,8 +322,23 @@ __device__ __forceinline__ void rollout_lane_glds(const Consts& K, const double*
         }
         v2 = g_ring[wv][u][0][lane];
         b2 = g_ring[wv][u][1][lane];
-        step_core<INTEG, ROT, PL2>(x[0], y[0], ph[0], sn[0], cs[0], v2.x, b2.x, K, bad[0]);
-        step_core<INTEG, ROT, PL2>(x[1], y[1], ph[1], sn[1], cs[1], v2.y, b2.y, K, bad[1]);
+#if MPC_EXPERIMENT == 1
+        x[0] += v2.x * b2.x;
+        x[1] += v2.y * b2.y;
+        continue;
+#elif MPC_EXPERIMENT == 2
+        v2 = make_double2(0.5 + 1e-3 * ((c0 + st) & 15), 0.5 + 1e-3 * ((c0 + 1 + st) & 15));
+        b2 = make_double2(0.01 * ((c0 >> 4) & 31) - 0.15, 0.01 * (((c0 + 1) >> 4) & 31) - 0.15);
+#endif
+        // the heading itself is not needed here (rotation mode carries sin/cos;
+        // an irregular candidate is recomputed from K.phi), so no phi chain
+        double ph0 = ROT ? 0.0 : ph[0], ph1 = ROT ? 0.0 : ph[1];
+        step_core<INTEG, ROT, PL2>(x[0], y[0], ph0, sn[0], cs[0], v2.x, b2.x, K, bad[0], &lead);
+        step_core<INTEG, ROT, PL2>(x[1], y[1], ph1, sn[1], cs[1], v2.y, b2.y, K, bad[1], &lead);
+        if (!ROT) {
+          ph[0] = ph0;
+          ph[1] = ph1;
+        }
       }
     }
   }

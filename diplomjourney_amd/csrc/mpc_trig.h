@@ -70,9 +70,14 @@ MPC_HD inline double fma_k(double a, double b, double c) {
 #endif
 }
 
+// `lead` is c[0].  Horner's first step fma(c0, z, c1) has two coefficient
+// operands, and gfx9 VALU instructions read at most one SGPR, so c0 has to be
+// in a VGPR: hipcc re-materialises it with a v_mov per evaluation unless the
+// caller passes a copy it keeps resident (see Leads).
 template <int N>
-MPC_HD inline double horner(const double (&c)[N], double z, int skip_last = 0) {
-  double p = c[0];
+MPC_HD inline double horner(const double (&c)[N], double z, int skip_last = 0,
+                            double lead = 0.0, bool have_lead = false) {
+  double p = have_lead ? lead : c[0];
 #pragma unroll
   for (int i = 1; i < N; ++i)
     if (i < N - skip_last) p = fma_k(p, z, c[i]);
@@ -157,10 +162,17 @@ constexpr double kTP[4] = {-0x1.5a006cab24f4bp-20, 0x1.88ebe003d6902p-12, -0x1.8
 constexpr double kTQ[5] = {0x1.61e9925b7b933p-20, -0x1.a739351555585p-12, 0x1.c2364f9313e10p-6,
                            -0x1.e1f1a9c96dd06p-2, 0x1.0000000000000p+0};
 
-MPC_HD inline double tan_small(double x) {
+// Leading polynomial coefficients of the hot loop's trig, held in VGPRs by
+// the rollout kernel (one copy per lane instead of a v_mov per use); equal to
+// the constants, so results are bitwise those of the default arguments.
+struct Leads {
+  double tp, tq, rs, rc;
+};
+
+MPC_HD inline double tan_small(double x, const Leads* ld = nullptr) {
   const double s = x * x;
-  const double p = horner(kTP, s);
-  const double q = horner(kTQ, s);        // in [0.59, 1]
+  const double p = ld ? horner(kTP, s, 0, ld->tp, true) : horner(kTP, s);
+  const double q = ld ? horner(kTQ, s, 0, ld->tq, true) : horner(kTQ, s);   // in [0.59, 1]
 #if defined(__HIP_DEVICE_COMPILE__)
   double r = __builtin_amdgcn_rcp(q);
 #else
@@ -227,11 +239,17 @@ constexpr double kRC[4] = {-0x1.27b71672cf54cp-22, 0x1.a019fd094f3a7p-16, -0x1.6
 
 // sd = sin(d), cm1 = cos(d) - 1 for |d| <= kRotMax (larger increments make
 // the candidate irregular: it is recomputed with direct evaluation)
-MPC_HD inline void rotation_factors(double d, double& sd, double& cm1) {
+// cm1 = z * (-1/2 + z * RC(z)): the -1/2 enters as an fma addend (inline
+// constant), one multiply fewer than -z/2 + z^2 * RC(z); its rounding of
+// -1/2 + z*RC adds at most 2^-54 relative, far below cm1's weight in c'.
+MPC_HD inline void rotation_factors(double d, double& sd, double& cm1,
+                                    const Leads* ld = nullptr) {
   const double z = d * d;
-  sd = fma(d * z, horner(kRS, z), d);
-  cm1 = fma(z * z, horner(kRC, z), -0.5 * z);
+  sd = fma(d * z, ld ? horner(kRS, z, 0, ld->rs, true) : horner(kRS, z), d);
+  cm1 = z * fma(z, ld ? horner(kRC, z, 0, ld->rc, true) : horner(kRC, z), -0.5);
 }
+
+MPC_HD inline Leads const_leads() { return Leads{kTP[0], kTQ[0], kRS[0], kRC[0]}; }
 
 // (s, c) <- rotation of (s, c) by the angle whose factors are (sd, cm1)
 MPC_HD inline void rotate_by(double sd, double cm1, double& s, double& c) {
