@@ -180,7 +180,9 @@ MPC_HD inline double tan_small(double x, const Leads* ld = nullptr) {
 #endif
   r = fma(r, fma(-q, r, 1.0), r);
   double R = p * r;
+#ifndef MPC_TAN_NOCORR
   R = fma(r, fma(-q, R, p), R);           // quotient correction
+#endif
   return fma(x * s, R, x);
 }
 
