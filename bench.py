@@ -24,7 +24,8 @@ host synchronisation inside the loop):
       grid), then the same two kernels
 On G > 1 GPUs the per-rank winners are exchanged with one RCCL all_gather
 before the episode update.  `value` is timed over K steps replayed from a HIP
-graph (one GPU) or launched eagerly (G > 1); p50/p90 come from a separate
+graph (the RCCL all_gather captured with the kernels on G > 1; gloo
+rehearsals launch eagerly); p50/p90 come from a separate
 eager pass with HIP events; `other_inputs` repeats the run with the other
 input mode.  --host-loop runs the host-driven episode instead.
 
@@ -98,6 +99,10 @@ def parse():
                     help="skip the comparison run with the other --inputs mode")
     ap.add_argument("--no-graph", action="store_true",
                     help="time eagerly launched steps instead of a HIP graph replay")
+    ap.add_argument("--exchange", action="store_true",
+                    help="use the multi-GPU step structure (finalize -> RCCL all_gather -> "
+                         "advance) even on one rank: rehearses the exchange and its graph "
+                         "capture on a single GPU (1-rank process group)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks on fewer GPUs (exchange staged via host)")
     ap.add_argument("--candidates-per-gpu", type=int, default=None,
@@ -170,7 +175,9 @@ def main():
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
     group = None
-    if world > 1:
+    if world > 1 or args.exchange:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
         else:
@@ -188,16 +195,23 @@ def main():
     from diplomjourney_amd.episode import DeviceEpisode, Episode, percentile
     n_total = (args.candidates_per_gpu or wl["per_gpu"]) * world
     n_steps = wl["n_steps"]
-    use_graph = world == 1 and not args.host_loop and not args.no_graph
+    exchange = world > 1 or args.exchange
+    # one GPU: the K steps are one HIP graph; with the exchange the RCCL
+    # all_gather is captured into the same graph (gloo stages through the
+    # host and cannot be captured)
+    use_graph = (not args.host_loop and not args.no_graph
+                 and (not exchange or args.dist_backend == "nccl"))
     inputs = "sampled" if args.host_loop else args.inputs
     if args.host_loop:
         ep = Episode(eng, n_total, n_steps, rank=rank, world=world,
                      integrator=args.integrator, group=group)
     else:
         ep = DeviceEpisode(eng, n_total, n_steps, rank=rank, world=world,
-                           integrator=args.integrator, group=group, log_capacity=8192)
+                           integrator=args.integrator, group=group, log_capacity=8192,
+                           exchange=exchange)
     pool = make_pool(eng, ep, n_steps, args.steps) if inputs == "resident" else None
     main_run = run_steps(args, ep, pool, use_graph, world, device)
+    use_graph = main_run["graph"]
     kern_ms = main_run["kernel_in_step_ms"]
     if hasattr(ep, "partials"):
         kern_ms = kernel_pass(ep, pool if pool is not None else
@@ -236,9 +250,11 @@ def main():
                    "integrator": args.integrator, "inputs": INPUTS_DOC[inputs],
                    "episodes_started": episodes,
                    "episode_loop": "host" if args.host_loop else "device-resident",
-                   "launch": "hipGraph of the K steps" if use_graph else "eager",
+                   "launch": (("hipGraph of the K steps" + (" incl. the RCCL all_gather"
+                                                             if exchange else ""))
+                              if use_graph else "eager"),
                    "parallelism": f"candidate-sharded x{world}" + (", all_gather(808 B)/step"
-                                                                   if world > 1 else "")},
+                                                                   if exchange else "")},
         "p50_ms": main_run["p50_ms"], "p90_ms": main_run["p90_ms"],
         "p50_note": "GPU time per MPC step (HIP events between step starts, eager launches)",
         "kernel_ms": kern_ms, "kernel_in_step_ms": main_run["kernel_in_step_ms"],
@@ -248,7 +264,7 @@ def main():
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if world > 1 or args.exchange:
         dist.destroy_process_group()
 
 
@@ -305,17 +321,25 @@ def run_steps(args, ep, pool, use_graph, world, device):
     step_gpu_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)]
     # Throughput pass: the K steps captured once into a HIP graph (the episode
     # lives in HBM, so a replay simply continues it) and replayed: no host
-    # cost between the step's kernels.  Multi-GPU runs launch eagerly (the
-    # RCCL exchange stays outside graph capture).
+    # cost between the step's kernels.  Multi-GPU runs capture the RCCL
+    # all_gather into the same graph (nccl backend; gloo runs launch eagerly).
     graph = None
     if use_graph:
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            for i in range(args.steps):
-                step(i)
-        ep.steps_enqueued -= args.steps      # captured, not run
-        graph.replay()                       # untimed: first replay
-        ep.steps_enqueued += args.steps
+        n0 = ep.steps_enqueued
+        try:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                for i in range(args.steps):
+                    step(i)
+        except Exception as e:   # capture refused (e.g. by the collective): launch eagerly
+            print(f"bench: graph capture failed ({type(e).__name__}: {e}); eager launches",
+                  file=sys.stderr, flush=True)
+            graph = None
+            torch.cuda.synchronize()
+        ep.steps_enqueued = n0               # captured, not run
+        if graph is not None:
+            graph.replay()                   # untimed: first replay
+            ep.steps_enqueued += args.steps
         torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -335,7 +359,8 @@ def run_steps(args, ep, pool, use_graph, world, device):
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    return {"elapsed": elapsed, "p50_ms": percentile(step_gpu_ms, 50),
+    return {"elapsed": elapsed, "graph": graph is not None,
+            "p50_ms": percentile(step_gpu_ms, 50),
             "p90_ms": percentile(step_gpu_ms, 90),
             "kernel_in_step_ms": sum(a.elapsed_time(b) for a, b in kern) / len(kern)}
 

@@ -178,7 +178,7 @@ class DeviceEpisode:
 
     def __init__(self, engine, n_cand_total, n_steps, rank=0, world=1, seed=20261015,
                  integrator="rect", group=None, start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3),
-                 log_capacity=4096, split=True):
+                 log_capacity=4096, split=True, exchange=None):
         self.eng = engine
         self.lib = native.lib()
         self.n_total = int(n_cand_total)
@@ -203,6 +203,12 @@ class DeviceEpisode:
         self._integ = INTEGRATORS[integrator]
         self.cur = (self.v_sc, self.b_sc)
         self.split = bool(split)
+        # exchange: the multi-GPU step structure (finalize -> all_gather ->
+        # advance).  Always on for world > 1; forcing it on one rank rehearses
+        # the RCCL exchange (and its HIP-graph capture) on a single GPU.
+        self.exchange = world > 1 if exchange is None else bool(exchange)
+        if world > 1 and not self.exchange:
+            raise ValueError("world > 1 needs the exchange step")
         self.steps_enqueued = 0
         self.reset()
 
@@ -238,7 +244,7 @@ class DeviceEpisode:
                 raise ValueError("controls must be contiguous float64 [n_steps, n_local] "
                                  "tensors on the episode's device")
             self.cur = (v, b)
-        one_gpu = self.world == 1    # one GPU: the step's launch also advances the episode
+        one_gpu = not self.exchange  # one GPU: the step's launch also advances the episode
         args = (self.state.data_ptr(), self.cur[0].data_ptr(), self.cur[1].data_ptr(),
                 self.n_local, self.n_steps, self.lo, self._integ, self.ws.data_ptr(),
                 self.ws.numel(), self.local.data_ptr(),
@@ -272,7 +278,7 @@ class DeviceEpisode:
         """Multi-GPU: all_gather of the per-rank winners (RCCL) + selection +
         episode update in one launch; no host synchronisation.  (On one GPU
         the update already ran inside finalize.)"""
-        if self.world == 1:
+        if not self.exchange:
             return
         gathered = gather_results(self.local, self.group)
         native.check(self.lib.mpc_episode_advance(

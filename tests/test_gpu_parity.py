@@ -346,3 +346,46 @@ def test_device_episode_resident_controls(engine, integ):
         idx_a, idx_b = a[1::2], b[1::2]
         assert torch.equal(idx_a, idx_b)
         x, y, phi = log.x, log.y, log.phi
+
+
+def test_device_episode_exchange_path_and_graph_capture(engine):
+    """The multi-GPU step structure (finalize -> RCCL all_gather -> advance)
+    over a 1-rank nccl group, launched eagerly and replayed from a HIP graph
+    that captures the collective, logs exactly the steps of the single-GPU
+    episode (finalize applies the update itself) on the same resident batches."""
+    import torch.distributed as dist
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.episode import DeviceEpisode
+    n, ns, steps = 40_000, 10, 12
+    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
+    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
+    pool = [engine.sample_controls(V, B, n, ns, 900 + i) for i in range(steps)]
+    ref = DeviceEpisode(engine, n, ns, log_capacity=64)
+    for i in range(steps):
+        ref.step(controls=pool[i])
+    want = [(r.step, r.index, r.cost, r.x, r.y, r.phi, r.v, r.beta) for r in ref.read_log()]
+    own = not dist.is_initialized()
+    if own:
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        eager = DeviceEpisode(engine, n, ns, log_capacity=64, exchange=True)
+        half = steps // 2
+        for i in range(half):                      # eager (also creates the communicator)
+            eager.step(controls=pool[i])
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):                  # the rest captured, collective included
+            for i in range(half, steps):
+                eager.step(controls=pool[i])
+        g.replay()
+        torch.cuda.synchronize()
+        got = [(r.step, r.index, r.cost, r.x, r.y, r.phi, r.v, r.beta) for r in eager.read_log()]
+        assert got == want
+    finally:
+        if own:
+            dist.destroy_process_group()
