@@ -195,7 +195,10 @@ def test_ties_resolve_to_lowest_index(engine):
     b = ((torch.rand((ns, n), generator=gen, dtype=torch.float64) - 0.5) * 2).cuda()
     engine.rollout_argmin(prob, v, b, incumbent=INC_MAX, integrator="rect")
     best = engine.fetch().index
-    for dup_at in (best + 1 if best + 1 < n else best - 1, 511, 512, n - 1, 0):
+    # positions across lane pairs, wave tiles (128), block tiles (512) and
+    # the launch's last, partial tile (700_000 = 1367 full tiles + 96)
+    for dup_at in (best + 1 if best + 1 < n else best - 1, 1, 127, 128, 129, 255, 256, 511, 512,
+                   1023, 1024, 699_391, 699_392, 699_393, n - 1, 0):
         v2, b2 = v.clone(), b.clone()
         v2[:, dup_at], b2[:, dup_at] = v[:, best], b[:, best]
         engine.rollout_argmin(prob, v2, b2, incumbent=INC_MAX, integrator="rect")
