@@ -30,8 +30,8 @@ eager pass with HIP events; `other_inputs` repeats the run with the other
 input mode.  --host-loop runs the host-driven episode instead.
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel
-(k_rollout_argmin): algorithmic bytes 16 B per candidate-step (fp64 v and
-beta read once) / its average duration, from HIP events around 20
+(k_rollout_argmin_stream): algorithmic bytes 16 B per candidate-step (fp64 v and
+beta read once) / its average duration, from HIP events around 100
 back-to-back launches on the episode's stream and controls.
 `cpu_baseline` is the reference-structured Python port (scipy quad) on this
 host's cores, rank 0 at N=1 only, on a bounded sample of the same candidates;
@@ -365,7 +365,7 @@ def run_steps(args, ep, pool, use_graph, world, device):
             "kernel_in_step_ms": sum(a.elapsed_time(b) for a, b in kern) / len(kern)}
 
 
-def kernel_pass(ep, pool, reps=20):
+def kernel_pass(ep, pool, reps=100):
     """The rollout kernel alone: REPS back-to-back launches between two HIP
     events on the launch stream, rotating over the resident batches (at least
     4 x the batch bytes between two uses of a batch, so no launch is served
@@ -398,7 +398,7 @@ def roofline(achieved, bytes_launch, traffic_json):
             traffic, src = t.get("hbm_bytes_per_launch"), os.path.relpath(traffic_json, REPO)
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
-            "kernel": "k_rollout_argmin", "algorithmic_bytes_per_launch": bytes_launch}
+            "kernel": "k_rollout_argmin_stream", "algorithmic_bytes_per_launch": bytes_launch}
 
 
 def bench_robots(args, wl, eng, rank, world, cpu):

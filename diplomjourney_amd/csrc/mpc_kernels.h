@@ -377,8 +377,8 @@ __device__ __forceinline__ void rollout_lane(const Consts& K, const double* __re
 }
 
 template <int CPL, int INTEG, bool ROT, bool STATES, bool KDEV>
-__global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(
-    Consts Karg, const Consts* __restrict__ Kdev, const double* __restrict__ v,
+__device__ __forceinline__ void rollout_argmin_body(
+    const Consts& Karg, const Consts* __restrict__ Kdev, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part,
     double* __restrict__ states) {
   const Consts K = KDEV ? *Kdev : Karg;
@@ -402,6 +402,31 @@ __global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(
   }
   block_argmin(best_k, best_i);
   if (threadIdx.x == 0) part[blockIdx.x] = Rec{best_k, best_i};
+}
+
+// Scalar (CPL = 1), CoordinateTree-states and register-ring paths.
+template <int CPL, int INTEG, bool ROT, bool STATES, bool KDEV>
+__global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(
+    Consts Karg, const Consts* __restrict__ Kdev, const double* __restrict__ v,
+    const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part,
+    double* __restrict__ states) {
+  rollout_argmin_body<CPL, INTEG, ROT, STATES, KDEV>(Karg, Kdev, v, b, n_cand, n_steps, part,
+                                                      states);
+}
+
+// The streaming kernel of the aligned path (CPL = 2, LDS-DMA ring).  With the
+// irregular-candidate recompute free of the device library's large-argument
+// trig (mpc_trig.h reduce_pio2_large), its registers fit kStreamWaves waves
+// per SIMD (5: <= 96 VGPRs; 6 spills).
+#ifndef MPC_STREAM_WAVES
+#define MPC_STREAM_WAVES 5
+#endif
+template <int INTEG, bool ROT, bool KDEV>
+__global__ __launch_bounds__(kBlock, MPC_STREAM_WAVES) void k_rollout_argmin_stream(
+    Consts Karg, const Consts* __restrict__ Kdev, const double* __restrict__ v,
+    const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part) {
+  rollout_argmin_body<kCplWide, INTEG, ROT, false, KDEV>(Karg, Kdev, v, b, n_cand, n_steps,
+                                                          part, nullptr);
 }
 
 // What the episode update needs of a winner (kept in registers by the

@@ -142,9 +142,8 @@ void launch_rollout(hipStream_t st, int32_t integrator, const Consts& K, const C
     constexpr int I = decltype(integ)::value;
     constexpr bool R = decltype(rot)::value;
     if (wide)
-      k_rollout_argmin<kCplWide, I, R, false, KDEV>
-          <<<rollout_grid<kCplWide>(n_cand), kBlock, 0, st>>>(
-              K, Kdev, v, b, n_cand, n_steps, part, nullptr);
+      k_rollout_argmin_stream<I, R, KDEV><<<rollout_grid<kCplWide>(n_cand), kBlock, 0, st>>>(
+          K, Kdev, v, b, n_cand, n_steps, part);
     else
       k_rollout_argmin<1, I, R, false, KDEV>
           <<<rollout_grid<1>(n_cand), kBlock, 0, st>>>(

@@ -9,7 +9,8 @@
 // producing a double-double remainder, followed by near-minimax polynomials on
 // |r| <= pi/4 (coefficients from tools/fit_trig.py, mpmath).  Arguments beyond
 // the Cody-Waite range take a (wave-divergent, in practice never taken) branch
-// to the library routine, so results are correct for every input.
+// to an integer Payne-Hanek reduction (reduce_pio2_large), so results are
+// correct for every input without the device library's large-argument code.
 //
 // Accuracy: faithful (< 1 ulp); see tests/test_trig.py for the measured error
 // against mpmath and the agreement rate with glibc (which the reference uses).
@@ -18,6 +19,7 @@
 #pragma once
 
 #include <math.h>
+#include <stdint.h>
 
 #if defined(__HIPCC__)
 #define MPC_HD __host__ __device__
@@ -194,8 +196,129 @@ MPC_HD inline double tan_core(double x) {
   return x == 0.0 ? x : t;  // tan(+-0) = +-0
 }
 
+MPC_HD inline void sincos_reduced(const Reduced& r, double* s, double* c);
+
 MPC_HD inline void sincos_core(double x, double* s, double* c) {
-  const Reduced r = reduce_pio2(x);
+  sincos_reduced(reduce_pio2(x), s, c);
+}
+
+// ---------------------------------------------------------------------------
+// Payne-Hanek reduction for |x| > kFastMax (up to DBL_MAX), in integer
+// arithmetic.  It replaces the device library's large-argument path, whose
+// inlined code set the VGPR budget of every kernel that can meet such an
+// argument (the rollout kernel's irregular-candidate recompute: 121 VGPRs
+// with it, ~92 without), and it is the same code on the host.
+//
+// x = m * 2^e (m the 53-bit significand).  With 2/pi = sum_i W[i] 2^-32(i+1)
+// (kTwoOverPiBits, tools/fit_trig.py --two-over-pi), the words with
+// e - 32(i+1) >= 2 only add multiples of 4 to x*2/pi and are skipped; the next
+// eight words (256 bits) give x*2/pi mod 4 with an absolute error below
+// 2^-138, i.e. 2^-77 relative to the smallest reduced argument a double can
+// produce (~2^-61).  Two leading zero words let the window start before the
+// binary point (e >= -33 here).
+constexpr uint32_t kTwoOverPiBits[40] = {
+    0x00000000, 0x00000000, 0xa2f9836e, 0x4e441529, 0xfc2757d1, 0xf534ddc0,
+    0xdb629599, 0x3c439041, 0xfe5163ab, 0xdebbc561, 0xb7246e3a, 0x424dd2e0,
+    0x06492eea, 0x09d1921c, 0xfe1deb1c, 0xb129a73e, 0xe88235f5, 0x2ebb4484,
+    0xe99c7026, 0xb45f7e41, 0x3991d639, 0x835339f4, 0x9c845f8b, 0xbdf9283b,
+    0x1ff897ff, 0xde05980f, 0xef2f118b, 0x5a0a6d1f, 0x6d367ecf, 0x27cb09b7,
+    0x4f463f66, 0x9e5fea2d, 0x7527bac7, 0xebe5f17b, 0x3d0739f7, 0x8a5292ea,
+    0x6bfb5fb1, 0x1f8d5d08, 0x56033046, 0xfc7b6bab,
+};
+
+MPC_HD inline void umul64wide(uint64_t a, uint64_t b, uint64_t& hi, uint64_t& lo) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  hi = __umul64hi(a, b);
+  lo = a * b;
+#else
+  const unsigned __int128 p = static_cast<unsigned __int128>(a) * b;
+  hi = static_cast<uint64_t>(p >> 64);
+  lo = static_cast<uint64_t>(p);
+#endif
+}
+
+// x finite, |x| > kFastMax: x = q*pi/2 + (hi + lo), |hi + lo| <= pi/4.
+MPC_HD inline Reduced reduce_pio2_large(double x) {
+  uint64_t bits;
+  __builtin_memcpy(&bits, &x, 8);
+  const bool neg = (bits >> 63) != 0;
+  const int e = static_cast<int>((bits >> 52) & 0x7ff) - 1075;          // x = m * 2^e
+  const uint64_t m = (bits & 0x000fffffffffffffull) | 0x0010000000000000ull;
+  const int i0 = ((e + 30) >> 5) + 1;               // first word used (+2: the zero words)
+  auto w64 = [&](int k) {
+    return (static_cast<uint64_t>(kTwoOverPiBits[i0 + 2 * k]) << 32) |
+           kTwoOverPiBits[i0 + 2 * k + 1];
+  };
+  // P = m * (w0 w1 w2 w3): limbs R1 (bits 192..255), R2, R3 (bits 64..127);
+  // the binary point of x*2/pi sits at bit 32*(i0-2+8) - e of P, in [223, 255).
+  uint64_t h0, l0, h1, l1, h2, l2, h3, l3;
+  umul64wide(m, w64(0), h0, l0);
+  umul64wide(m, w64(1), h1, l1);
+  umul64wide(m, w64(2), h2, l2);
+  umul64wide(m, w64(3), h3, l3);
+  (void)h0;
+  (void)l3;
+  const uint64_t R3 = h3 + l2;
+  const uint64_t c3 = R3 < l2 ? 1 : 0;
+  uint64_t R2 = h2 + l1;
+  uint64_t c2 = R2 < l1 ? 1 : 0;
+  R2 += c3;
+  c2 += (R2 < c3) ? 1 : 0;
+  const uint64_t R1 = h1 + l0 + c2;
+  const int t = 32 * (i0 + 6) - e - 192;            // binary point at bit 192 + t, t in [31, 63)
+  const uint64_t F_hi = (R2 >> t) | (R1 << (64 - t));   // the 128 fraction bits
+  const uint64_t F_lo = (R3 >> t) | (R2 << (64 - t));
+  int q = static_cast<int>((R1 >> t) & 3);
+  // fraction f in [0, 1) -> [-1/2, 1/2): above 1/2 take f - 1 and q + 1
+  double fh, fl;
+  const double k2m64 = 0x1p-64;
+  if (F_hi >> 63) {
+    const uint64_t nlo = ~F_lo + 1;                 // 2^128 - F
+    const uint64_t nhi = ~F_hi + (nlo == 0 ? 1 : 0);
+    q += 1;
+    const double a = static_cast<double>(nhi);      // rounded; the rest is exact below
+    const uint64_t ai = static_cast<uint64_t>(a);
+    const double r = static_cast<double>(static_cast<int64_t>(nhi - ai)) +
+                     static_cast<double>(nlo) * k2m64;
+    fh = -(a * k2m64);
+    fl = -(r * k2m64);
+  } else {
+    const double a = static_cast<double>(F_hi);
+    const uint64_t ai = static_cast<uint64_t>(a);
+    const double r = static_cast<double>(static_cast<int64_t>(F_hi - ai)) +
+                     static_cast<double>(F_lo) * k2m64;
+    fh = a * k2m64;
+    fl = r * k2m64;
+  }
+  const double s0 = fh + fl;                        // normalise the fraction
+  fl = fl - (s0 - fh);
+  fh = s0;
+  // (fh + fl) * pi/2 in double-double
+  constexpr double kPio2Hi = 0x1.921fb54442d18p+0, kPio2Lo = 0x1.1a62633145c07p-54;
+  const double ph = fh * kPio2Hi;
+  const double pl = fma(fh, kPio2Hi, -ph) + (fh * kPio2Lo + fl * kPio2Hi);
+  Reduced o;
+  o.hi = ph + pl;
+  o.lo = pl - (o.hi - ph);
+  o.q = q;
+  if (neg) {
+    o.hi = -o.hi;
+    o.lo = -o.lo;
+    o.q = -q;
+  }
+  return o;
+}
+
+// Full forms: any argument.  |x| <= kFastMax: the Cody-Waite cores; larger
+// finite x: Payne-Hanek; inf / NaN: NaN.
+MPC_HD inline double tan_fast(double x) {
+  if (fabs(x) <= kFastMax) return tan_core(x);
+  if (!(fabs(x) < __builtin_inf())) return x - x;
+  const Reduced r = reduce_pio2_large(x);
+  return ktan(r.hi, r.lo, (r.q & 1) != 0);
+}
+
+MPC_HD inline void sincos_reduced(const Reduced& r, double* s, double* c) {
   const double sn = ksin(r.hi, r.lo);
   const double cs = kcos(r.hi, r.lo);
   const int q = r.q & 3;
@@ -207,19 +330,16 @@ MPC_HD inline void sincos_core(double x, double* s, double* c) {
   *c = C;
 }
 
-// Full forms: any argument (huge or non-finite ones go to the library).
-MPC_HD inline double tan_fast(double x) {
-  if (!(fabs(x) <= kFastMax)) return ::tan(x);
-  return tan_core(x);
-}
-
 MPC_HD inline void sincos_fast(double x, double* s, double* c) {
-  if (!(fabs(x) <= kFastMax)) {
-    *s = ::sin(x);
-    *c = ::cos(x);
+  if (fabs(x) <= kFastMax) {
+    sincos_core(x, s, c);
     return;
   }
-  sincos_core(x, s, c);
+  if (!(fabs(x) < __builtin_inf())) {
+    *s = *c = x - x;
+    return;
+  }
+  sincos_reduced(reduce_pio2_large(x), s, c);
 }
 
 // ---------------------------------------------------------------------------

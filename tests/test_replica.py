@@ -86,3 +86,40 @@ def test_gpu_bitwise_equals_replica(engine, n, ns, integ):
     fast = engine.fetch()
     assert fast.index == k and fast.cost == costs[k]
     assert fast.trajectory() == [list(st[s, :, k]) for s in range(ns)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("integ", ["rect+rot", "rect", "qk21", "qk21+rot"])
+def test_gpu_irregular_candidates_stream_kernel(engine, integ):
+    """Irregular candidates (|beta| > 1.1 at some step; in rotation mode also
+    |dphi| > 0.2) leave the streaming kernel's fast loop and are recomputed
+    with the safe recurrence (full-range trig) in the same lane.  Winner,
+    cost and trajectory equal the host replica bit for bit: (a) most
+    candidates irregular, irregular winner; (b) a few irregular candidates
+    scattered over otherwise regular blocks; (c) 2.1e6 candidates, so blocks
+    stride over several tiles, with irregular candidates only in late tiles."""
+    from diplomjourney_amd.abi import make_problem
+    rng = np.random.default_rng(3)
+    p = make_problem(0, 0, 0, 0.3, 0.8, 0, 0, 0.5, 0.05, 0.1)
+    cases = []
+    n, ns = 200_000, 10
+    cases.append((rng.uniform(0, 1, (ns, n)), rng.uniform(-1.25, 1.25, (ns, n)), True))
+    v, b = _case(n, ns, 12)
+    hit = rng.choice(n, 40, replace=False)
+    b[rng.integers(0, ns, 40), hit] = 1.2
+    cases.append((v, b, None))
+    n = 2 * 2048 * 512 + 1000
+    v, b = _case(n, 4, 13)
+    b[2, [2048 * 512 + 7, n - 3, n - 600]] = -1.15
+    cases.append((v, b, None))
+    for v, b, want_irregular in cases:
+        st, costs = replica_rollout(p, v, b, integ)
+        k = int(np.argmin(costs))
+        if want_irregular:
+            assert np.abs(b[:, k]).max() > 1.1       # the case exercises an irregular winner
+        engine.rollout_argmin(p, torch.as_tensor(v, device="cuda"),
+                              torch.as_tensor(b, device="cuda"), incumbent=INC_MAX,
+                              integrator=integ)
+        got = engine.fetch()
+        assert got.index == k and got.cost == costs[k]
+        assert got.trajectory() == [list(st[s, :, k]) for s in range(v.shape[0])]

@@ -43,6 +43,28 @@ def test_agreement_with_glibc():
         assert np.all(np.abs(out - g) <= np.spacing(np.abs(g)))
 
 
+def test_payne_hanek_faithful_against_mpmath():
+    """Arguments beyond the Cody-Waite range (|x| > 2^19*pi/2) take the
+    kernel's own Payne-Hanek reduction (reduce_pio2_large): faithful against
+    mpmath from 1e6 to DBL_MAX, incl. the double closest to a multiple of
+    pi/2 (6381956970095103 * 2^797, remainder ~4.7e-19) and arguments just
+    beyond the switch-over."""
+    mp.mp.prec = 2200                    # exact reduction of arguments up to 2^1024
+    rng = np.random.default_rng(9)
+    x = np.concatenate([
+        rng.uniform(1, 2, 1500) * 2.0 ** rng.integers(20, 1024, 1500),
+        [math.ldexp(6381956970095103, 797), 2.0 ** 19 * math.pi / 2 * (1 + 2 ** -52),
+         823550.0, 1e22, 2.0 ** 1023 * (2 - 2 ** -52), 3.0 * 2 ** 60]])
+    x = np.concatenate([x, -x])
+    t, s, c = trig_eval(x)
+    worst = [max(_ulp_err(g, xi, fn) for g, xi in zip(out, x))
+             for out, fn in ((t, mp.tan), (s, mp.sin), (c, mp.cos))]
+    assert max(worst) < 1.0, worst
+    agree = [np.mean(out == np.array([f(v) for v in x]))
+             for out, f in ((t, _m.tan), (s, _m.sin), (c, _m.cos))]
+    assert min(agree) > 0.85, agree
+
+
 def test_special_values():
     x = np.array([0.0, -0.0, 5e-324, -5e-324, 1e-300, math.pi / 2, 1e6, -1e6, 1e7, 3e9,
                   math.inf, -math.inf, math.nan])

@@ -141,3 +141,15 @@ def fit_tan_rational(xmax=1.1, m=3, n=4, iters=40, nodes=240):
 
 if __name__ == "__main__" and "--tan-rational" in __import__("sys").argv:
     fit_tan_rational()
+
+
+def two_over_pi_words(n=38):
+    """2/pi as n big-endian 32-bit words of its binary fraction (the
+    Payne-Hanek table of mpc_trig.h, kTwoOverPiBits)."""
+    mp.mp.prec = 32 * n + 64
+    v = int(mp.floor(2 / mp.pi * mp.mpf(2) ** (32 * n)))
+    return [(v >> (32 * (n - 1 - i))) & 0xffffffff for i in range(n)]
+
+
+if __name__ == "__main__" and "--two-over-pi" in __import__("sys").argv:
+    print(", ".join("0x%08x" % w for w in two_over_pi_words()))
