@@ -83,10 +83,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="C", choices=sorted(WORKLOADS))
     ap.add_argument("--integrator", default="rect+rot",
-                    choices=["rect+rot", "rect", "qk21+rot", "qk21"],
+                    choices=["rect+cum", "rect+rot", "rect", "qk21+rot", "qk21"],
                     help="kernel arithmetic (DESIGN.md 'Integrators'): qk21 = the reference's "
                          "quad() bit for bit, rect = direct h*f; +rot = heading carried as "
-                         "(sin, cos) and rotated per step")
+                         "(sin, cos) and rotated per step; +cum = rotated from the identity, "
+                         "start pose applied last (enables chained steps)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="per-core time budget of the cpu_baseline sample (0 = skip)")
     ap.add_argument("--host-loop", action="store_true",
@@ -97,6 +98,9 @@ def parse():
                          "input); sampled: the device sampler regenerates them per step")
     ap.add_argument("--no-second-pass", action="store_true",
                     help="skip the comparison run with the other --inputs mode")
+    ap.add_argument("--no-chain", action="store_true",
+                    help="separate selection launch per step instead of chained steps "
+                         "(mpc_episode_chain_step: the step's launch completes the previous step)")
     ap.add_argument("--no-graph", action="store_true",
                     help="time eagerly launched steps instead of a HIP graph replay")
     ap.add_argument("--exchange", action="store_true",
@@ -208,7 +212,7 @@ def main():
     else:
         ep = DeviceEpisode(eng, n_total, n_steps, rank=rank, world=world,
                            integrator=args.integrator, group=group, log_capacity=8192,
-                           exchange=exchange)
+                           exchange=exchange, chain=not args.no_chain)
     pool = make_pool(eng, ep, n_steps, args.steps) if inputs == "resident" else None
     main_run = run_steps(args, ep, pool, use_graph, world, device)
     use_graph = main_run["graph"]
@@ -253,6 +257,12 @@ def main():
                    "launch": (("hipGraph of the K steps" + (" incl. the RCCL all_gather"
                                                              if exchange else ""))
                               if use_graph else "eager"),
+                   "step_launches": (("chained: rollout of step k + completion of step k-1 in "
+                                      "one launch" + (" (+ local finalize + all_gather)"
+                                                      if exchange else ""))
+                                     if getattr(ep, "chain", False) and inputs == "resident"
+                                     else "rollout, then selection" + (
+                                         " + all_gather + advance" if exchange else "")),
                    "parallelism": f"candidate-sharded x{world}" + (", all_gather(808 B)/step"
                                                                    if exchange else "")},
         "p50_ms": main_run["p50_ms"], "p90_ms": main_run["p90_ms"],
@@ -307,8 +317,10 @@ def run_steps(args, ep, pool, use_graph, world, device):
         else:
             ep.step(events=events, controls=pool[i % len(pool)])
 
+    flush = getattr(ep, "flush", lambda: None)   # completes a chained step left pending
     for i in range(args.warmup):
         step(i)
+    flush()
     Ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     kern = [(Ev(), Ev()) for _ in range(args.steps)]
     marks = [Ev() for _ in range(args.steps + 1)]
@@ -317,6 +329,7 @@ def run_steps(args, ep, pool, use_graph, world, device):
         marks[i].record()
         step(i, kern[i])
     marks[-1].record()
+    flush()
     torch.cuda.synchronize()
     step_gpu_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)]
     # Throughput pass: the K steps captured once into a HIP graph (the episode
@@ -331,10 +344,13 @@ def run_steps(args, ep, pool, use_graph, world, device):
             with torch.cuda.graph(graph):
                 for i in range(args.steps):
                     step(i)
+                flush()                      # the K-th step completes inside the graph
         except Exception as e:   # capture refused (e.g. by the collective): launch eagerly
             print(f"bench: graph capture failed ({type(e).__name__}: {e}); eager launches",
                   file=sys.stderr, flush=True)
             graph = None
+            if hasattr(ep, "_pending"):
+                ep._pending = None           # the captured launches never ran
             torch.cuda.synchronize()
         ep.steps_enqueued = n0               # captured, not run
         if graph is not None:
@@ -351,6 +367,7 @@ def run_steps(args, ep, pool, use_graph, world, device):
     else:
         for i in range(args.steps):
             step(i)
+        flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -18,12 +18,15 @@ MPC_INTEG_QK21 = 0
 MPC_INTEG_RECT = 1
 
 MPC_HEADING_ROTATE = 0x100
+MPC_HEADING_CUMULATIVE = 0x200
 
 # integrator argument of the C ABI: QUADPACK-exact or exact integral, each
 # with the heading evaluated directly (reference formula) or by rotation
 INTEGRATORS = {"qk21": MPC_INTEG_QK21, "rect": MPC_INTEG_RECT,
                "qk21+rot": MPC_INTEG_QK21 | MPC_HEADING_ROTATE,
-               "rect+rot": MPC_INTEG_RECT | MPC_HEADING_ROTATE}
+               "rect+rot": MPC_INTEG_RECT | MPC_HEADING_ROTATE,
+               # rotation from the identity, start pose applied last (chained steps)
+               "rect+cum": MPC_INTEG_RECT | MPC_HEADING_CUMULATIVE}
 
 
 class MpcProblem(ctypes.Structure):

@@ -90,8 +90,16 @@ MPC_HD __forceinline__ double position_step(double p, double v, double trig, con
 // hot loop carries no fallback code.
 //   ROT = false: sin/cos of the new heading evaluated directly (the reference's
 //                formula, :113-114)
-//   ROT = true:  (s, c) carry sin/cos of the heading and are rotated by the
+//   ROT = 1:     (s, c) carry sin/cos of the heading and are rotated by the
 //                increment (mpc_trig.h rotation_factors / rotate_by)
+//   ROT = 2:     (kRotCum) the same recurrence started from the identity
+//                rotation (s, c) = (0, 1) and positions (x, y) = (0, 0): it
+//                accumulates the pose-independent sums A = sum vh cos(Phi_k),
+//                B = sum vh sin(Phi_k) of the heading increments Phi_k since
+//                the start; cum_pose() turns them into the pose.  The work
+//                per step is ROT = 1's; only the start state and the final
+//                transform differ, and nothing before the transform needs the
+//                start pose (the chained episode step, k_episode_chain).
 //   PL2:         L is a power of two (v / L == v * inv_L exactly).  A template
 //                parameter, not a branch: a branch inside the step would split
 //                the loop into basic blocks and stop the scheduler from
@@ -100,7 +108,7 @@ MPC_HD __forceinline__ double position_step(double p, double v, double trig, con
 //                value (scaling by a power of two commutes with rounding in the
 //                normal range) — so v * h is shared with the position update.
 //   ld:          VGPR-resident leading coefficients (trig::Leads), or nullptr.
-template <int INTEG, bool ROT, bool PL2>
+template <int INTEG, int ROT, bool PL2>
 MPC_HD __forceinline__ void step_core(double& x, double& y, double& ph, double& s, double& c,
                                       double v, double beta, const Consts& K, bool& bad,
                                       const trig::Leads* ld = nullptr) {
@@ -133,6 +141,33 @@ MPC_HD __forceinline__ void step_core(double& x, double& y, double& ph, double& 
   }
 }
 
+constexpr int kRotCum = 2;
+
+// Start state of the step recurrence: the pose (ROT 0 / 1) or the identity
+// rotation and empty sums (kRotCum).
+template <int ROT>
+MPC_HD __forceinline__ void step_start(const Consts& K, double& x, double& y, double& ph,
+                                       double& s, double& c) {
+  ph = K.phi;
+  if constexpr (ROT == kRotCum) {
+    x = 0.0;
+    y = 0.0;
+    s = 0.0;
+    c = 1.0;
+  } else {
+    x = K.x;
+    y = K.y;
+    s = K.s0;
+    c = K.c0;
+  }
+}
+
+// kRotCum: position from the sums, x = x0 + (c0 A - s0 B), y = y0 + (s0 A + c0 B)
+MPC_HD __forceinline__ void cum_pose(const Consts& K, double A, double B, double& x, double& y) {
+  x = K.x + fma(K.c0, A, -(K.s0 * B));
+  y = K.y + fma(K.s0, A, K.c0 * B);
+}
+
 template <int INTEG>
 MPC_HD __forceinline__ void step_safe(double& x, double& y, double& ph, double v, double beta,
                                       const Consts& K) {
@@ -162,18 +197,26 @@ MPC_HD __forceinline__ double cost(double x, double y, const Consts& K) {
 // tests/replica_harness.cpp calls this): the core recurrence, and if that
 // flags the candidate, the safe recurrence.  traj (optional) gets the
 // per-step (x, y, phi).  Returns the cost.
-template <int INTEG, bool ROT, bool PL2>
+template <int INTEG, int ROT, bool PL2>
 MPC_HD inline double rollout_candidate_l(const Consts& K, const double* v, const double* b,
                                          int64_t ld, int64_t col, int n_steps, double* traj) {
-  double x = K.x, y = K.y, ph = K.phi, s = K.s0, c = K.c0;
+  double x, y, ph, s, c;
+  step_start<ROT>(K, x, y, ph, s, c);
   bool bad = false;
   for (int st = 0; st < n_steps; ++st) {
     step_core<INTEG, ROT, PL2>(x, y, ph, s, c, v[st * ld + col], b[st * ld + col], K, bad);
     if (traj) {
-      traj[3 * st + 0] = x;
-      traj[3 * st + 1] = y;
+      if constexpr (ROT == kRotCum) {
+        cum_pose(K, x, y, traj[3 * st + 0], traj[3 * st + 1]);
+      } else {
+        traj[3 * st + 0] = x;
+        traj[3 * st + 1] = y;
+      }
       traj[3 * st + 2] = ph;
     }
+  }
+  if constexpr (ROT == kRotCum) {
+    if (!bad) cum_pose(K, x, y, x, y);
   }
   if (bad) {
     x = K.x;
@@ -191,7 +234,7 @@ MPC_HD inline double rollout_candidate_l(const Consts& K, const double* v, const
   return cost(x, y, K);
 }
 
-template <int INTEG, bool ROT>
+template <int INTEG, int ROT>
 MPC_HD inline double rollout_candidate(const Consts& K, const double* v, const double* b,
                                        int64_t ld, int64_t col, int n_steps, double* traj) {
   return K.L_pow2 ? rollout_candidate_l<INTEG, ROT, true>(K, v, b, ld, col, n_steps, traj)

@@ -15,11 +15,16 @@
 // finishing logic (:392-414), operator events (:564-569), arrival restart.
 #pragma once
 
+#include <stddef.h>
+
 #include "mpc_kernels.h"
 
 namespace mpc {
 
 constexpr int kEpMaxGrid = 64;
+constexpr int kConstsWords = static_cast<int>(sizeof(Consts) / 4);
+constexpr int kPubWords = kConstsWords + 2;   // Consts, then t
+static_assert(sizeof(Consts) % 4 == 0 && kPubWords <= 64, "published words: one wave");
 
 // EpisodeHead (mpc_kernels.h): the scalars; the grids only feed the sampler.
 struct EpisodeState {
@@ -27,7 +32,12 @@ struct EpisodeState {
   double grid_v[kEpMaxGrid];
   double grid_b[kEpMaxGrid];
   uint32_t done;       // blocks of the running fused launch that have finished
-  uint32_t pad_;
+  uint32_t chain_error;   // a chained step's wait timed out (k_episode_chain)
+  // Constants published by a chained launch's block 0 (k_episode_chain): the
+  // dwords of the step's Consts and of t, each in a 64-bit word tagged with
+  // the launch's epoch ((dword << 32) | epoch), so one coherent load per word
+  // says whether its value is this step's.  Tag 0: none.
+  alignas(128) uint64_t chain_pub[kPubWords];
 };
 
 __device__ inline Consts episode_consts(const EpisodeHead& S, double x, double y, double phi,
@@ -90,6 +100,8 @@ __global__ void k_episode_reset(mpc_episode_config_t c, EpisodeState* __restrict
   episode_prepare(c, H);
   S->h = H;
   S->done = 0u;
+  S->chain_error = 0u;
+  for (int q = 0; q < kPubWords; ++q) S->chain_pub[q] = 0ull;
 }
 
 // Grids (:239-256) with the reference's expressions and the slow-down
@@ -280,10 +292,9 @@ __device__ void episode_hook(const mpc_episode_config_t& c, const EpisodeHook& h
 
 // Multi-GPU: lexicographic (cost, global index) selection over the gathered
 // per-rank winners (the all-reduce(min+index)), then the episode update.
-__global__ void k_episode_advance(mpc_episode_config_t c, EpisodeState* __restrict__ S,
-                                  const mpc_result_t* __restrict__ res, int n,
-                                  mpc_episode_log_t* __restrict__ log, int cap) {
-  if (threadIdx.x != 0) return;
+__device__ inline void advance_from_results(const mpc_episode_config_t& c, EpisodeState* S,
+                                            const mpc_result_t* __restrict__ res, int n,
+                                            mpc_episode_log_t* __restrict__ log, int cap) {
   EpisodeHead H = S->h;
   uint64_t bk;
   const int best = select_index(res, n, bk);
@@ -299,6 +310,219 @@ __global__ void k_episode_advance(mpc_episode_config_t c, EpisodeState* __restri
     for (int q = 0; q < 3; ++q) w.tr[k][q] = r.traj[k < r.n_steps ? k : 0][q];
   episode_advance(c, H, w, log, cap);
   S->h = H;
+}
+
+__global__ void k_episode_advance(mpc_episode_config_t c, EpisodeState* __restrict__ S,
+                                  const mpc_result_t* __restrict__ res, int n,
+                                  mpc_episode_log_t* __restrict__ log, int cap) {
+  if (threadIdx.x != 0) return;
+  advance_from_results(c, S, res, n, log, cap);
+  for (int q = 0; q < kPubWords; ++q) S->chain_pub[q] = 0ull;   // ends a chain of chained steps
+}
+
+// ---------------------------------------------------------------------------
+// Chained episode step (heading mode kRotCum): ONE launch = this step's
+// streaming rollout + the completion of the PREVIOUS step.  Block 0 completes
+// step k-1 — kChainFin (one GPU): k_finalize's record reduction, winner
+// re-roll and episode update; kChainAdv (multi-GPU): k_episode_advance's
+// selection over the gathered per-rank winners and the update — and publishes
+// step k's constants as epoch-tagged words (EpisodeState::chain_pub).
+// The other blocks do not wait for it: in kRotCum mode a candidate's rollout
+// needs no start pose, only the step size h (and the constant wheelbase
+// terms).  A block reads the published words once, right after its first
+// control loads are in flight: if all carry this launch's epoch (block 0 is
+// done: every block after the first round) the constants are final; else it
+// speculates h as the next step of the same episode (from the previous
+// step's published t, + dt, as episode_prepare forms it) and reads the words
+// again after its loop, for the final pose transform and the criterion.  If h
+// turns out different (the previous step restarted the episode and reset t)
+// the lane recomputes with the published constants (rollout_lane_glds).
+// Records of tile-block b go to part[b - 1].  Consecutive chained launches
+// carry different epochs and the update that ends a chain (k_finalize's hook,
+// k_episode_advance) clears the tags.  The wait is bounded: if the words
+// never came, chain_error is set instead of hanging the GPU.
+constexpr int kChainFin = 1, kChainAdv = 2;
+constexpr uint32_t kChainSpinLimit = 1u << 17;   // x ~2k cycles: ~0.1 s
+
+// LDS dwords (Consts layout) -> wave-uniform Consts, field by field (no
+// memory view of the struct: it stays in SGPRs).
+__device__ __forceinline__ Consts consts_from_words(const uint32_t* w) {
+  auto d = [&](size_t off) {
+    const int q = static_cast<int>(off / 4);
+    // (readfirstlane returns int: through uint32_t, not sign-extended)
+    const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(w[q]));
+    const uint64_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(w[q + 1]));
+    return __longlong_as_double(static_cast<long long>((hi << 32) | lo));
+  };
+  auto i32 = [&](size_t off) {
+    return static_cast<int32_t>(__builtin_amdgcn_readfirstlane(w[off / 4]));
+  };
+  Consts K;
+  K.x = d(offsetof(Consts, x));
+  K.y = d(offsetof(Consts, y));
+  K.phi = d(offsetof(Consts, phi));
+  K.x_t = d(offsetof(Consts, x_t));
+  K.y_t = d(offsetof(Consts, y_t));
+  K.x_0 = d(offsetof(Consts, x_0));
+  K.y_0 = d(offsetof(Consts, y_0));
+  K.A = d(offsetof(Consts, A));
+  K.B = d(offsetof(Consts, B));
+  K.C1 = d(offsetof(Consts, C1));
+  K.C2 = d(offsetof(Consts, C2));
+  K.den = d(offsetof(Consts, den));
+  K.L = d(offsetof(Consts, L));
+  K.inv_L = d(offsetof(Consts, inv_L));
+  K.h = d(offsetof(Consts, h));
+  K.hlgth = d(offsetof(Consts, hlgth));
+  K.s0 = d(offsetof(Consts, s0));
+  K.c0 = d(offsetof(Consts, c0));
+  K.L_pow2 = i32(offsetof(Consts, L_pow2));
+  K.pad_ = 0;
+  return K;
+}
+
+// Block 0, all threads, after the episode head is stored: publish its Consts
+// and t as tagged words (relaxed agent-scope atomic stores: coherent, and each
+// word validates itself).
+__device__ __forceinline__ void chain_publish(EpisodeState* S, uint32_t epoch) {
+  __syncthreads();   // the head (stored by thread 0) is visible to the block
+  const int q = threadIdx.x;
+  if (q < kPubWords) {
+    const uint32_t d = q < kConstsWords
+                           ? reinterpret_cast<const uint32_t*>(&S->h.K)[q]
+                           : reinterpret_cast<const uint32_t*>(&S->h.t)[q - kConstsWords];
+    __hip_atomic_store(&S->chain_pub[q], (static_cast<uint64_t>(d) << 32) | epoch,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Wave 0 of a tile block: one coherent load of every published word into
+// s_w / s_tag; returns (wave-uniform) whether all carry `epoch`.
+__device__ __forceinline__ bool chain_read(const EpisodeState* S, uint32_t epoch,
+                                           uint32_t* s_w, uint32_t* s_tag) {
+  const int q = threadIdx.x;
+  bool ok = true;
+  if (q < kPubWords) {
+    const uint64_t w = __hip_atomic_load(const_cast<uint64_t*>(&S->chain_pub[q]),
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_w[q] = static_cast<uint32_t>(w >> 32);
+    s_tag[q] = static_cast<uint32_t>(w);
+    ok = static_cast<uint32_t>(w) == epoch;
+  }
+  return __ballot(!ok) == 0;
+}
+
+#ifndef MPC_CHAIN_WAVES
+#define MPC_CHAIN_WAVES 4   // launch bound of the chained kernel (5 spills: block 0's finalize)
+#endif
+template <int INTEG, int ROT, int MODE>
+__global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
+    EpisodeState* __restrict__ S, uint32_t epoch, const double* __restrict__ v,
+    const double* __restrict__ b, int64_t n_cand, int n_steps, int pl2, Rec* __restrict__ part,
+    int has_prev, const Rec* __restrict__ part_prev, int n_part_prev,
+    const double* __restrict__ v_prev, const double* __restrict__ b_prev, int64_t index_base,
+    mpc_result_t* __restrict__ out_prev, const mpc_result_t* __restrict__ gathered,
+    int n_gathered, mpc_episode_config_t ecfg, mpc_episode_log_t* __restrict__ log, int cap) {
+  static_assert(ROT == kRotCum, "chained steps need the pose-independent recurrence");
+  if (blockIdx.x == 0) {
+#ifdef MPC_CHAIN_NOFIN
+    has_prev = 0;   // A/B probe only
+#endif
+    if (has_prev) {
+      if constexpr (MODE == kChainFin) {
+        const Consts Kp = S->h.K;
+        const EpisodeHook hook{&S->h, log, cap, nullptr, 0};
+        finalize_block<INTEG, ROT, true, kBlock, false>(part_prev, n_part_prev, Kp, v_prev,
+                                                        b_prev, n_cand, n_steps, index_base,
+                                                        S->h.incumbent, out_prev, ecfg, hook);
+      } else {
+        if (threadIdx.x == 0) advance_from_results(ecfg, S, gathered, n_gathered, log, cap);
+      }
+    }
+    chain_publish(S, epoch);
+    return;
+  }
+  constexpr int CPL = 2;
+  __shared__ uint32_t s_w[kPubWords], s_tag[kPubWords];
+  __shared__ int s_final;
+  Consts Kl, K;
+  bool waited = false;
+  // After the block's first control loads are in flight: the loop constants.
+  // (K itself is formed only after the loop, from the LDS words, so that it
+  // is not live in SGPRs across the loop.)
+  auto pre0 = [&]() {
+    if (threadIdx.x < 64) {
+      bool fin = true;
+      if (has_prev) {
+        fin = chain_read(S, epoch, s_w, s_tag);
+      } else if (threadIdx.x < kConstsWords) {   // block 0 only republishes the head
+        s_w[threadIdx.x] = reinterpret_cast<const uint32_t*>(&S->h.K)[threadIdx.x];
+      }
+      if (threadIdx.x == 0) s_final = fin;
+    }
+    __syncthreads();
+    Kl = consts_from_words(s_w);
+    if (s_final) return;
+    // speculate h from the published t: the previous step's (+ dt) or, if
+    // block 0 already published it, this step's; torn -> NaN (recompute)
+    const uint32_t g0 = s_tag[kConstsWords], g1 = s_tag[kConstsWords + 1];
+    const uint64_t tb = (static_cast<uint64_t>(s_w[kConstsWords + 1]) << 32) | s_w[kConstsWords];
+    double t = __longlong_as_double(static_cast<long long>(tb));
+    if (g0 == g1 && g0 == epoch - 1u)
+      t = t + ecfg.delta_t;                                   // episode_prepare
+    else if (!(g0 == g1 && g0 == epoch))
+      t = __builtin_nan("");
+    Kl.h = (t + ecfg.delta_t) - t;                            // consts_from_problem: t_b - t_a
+  };
+  // After the loop: the final constants (called by every thread of the block
+  // at the same point, see the clamp below).
+  auto wait = [&]() {
+    if (waited) return;
+    waited = true;
+#ifdef MPC_CHAIN_NOWAIT
+    K = Kl;   // A/B probe only
+    return;
+#endif
+    __syncthreads();   // LDS reuse
+    if (!s_final) {
+      if (threadIdx.x < 64) {
+        uint32_t it = 0;
+        bool fin;
+        while (!(fin = chain_read(S, epoch, s_w, s_tag)) && ++it < kChainSpinLimit)
+          __builtin_amdgcn_s_sleep(32);
+        if (!fin && threadIdx.x == 0) S->chain_error = 1u;
+      }
+      __syncthreads();
+    }
+    K = consts_from_words(s_w);
+  };
+  const int64_t n_tiles = (n_cand + kBlock * CPL - 1) / (kBlock * CPL);
+  uint64_t best_k = ~0ull;
+  int64_t best_i = INT64_MAX;
+  for (int64_t tile = blockIdx.x - 1; tile < n_tiles; tile += gridDim.x - 1) {
+    const int64_t c0 = tile * (kBlock * CPL) + threadIdx.x * CPL;
+    // lanes past the end of a partial tile roll the last pair again (result
+    // ignored), so every lane reaches the barriers of pre0 / wait on the same path
+    const int64_t cl = c0 < n_cand ? c0 : n_cand - CPL;
+    double cst[CPL];
+    if (pl2)
+      rollout_lane_glds_k<INTEG, ROT, true>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0);
+    else
+      rollout_lane_glds_k<INTEG, ROT, false>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0);
+    Kl = K;            // later tiles: the final constants
+    if (c0 < n_cand) {
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        const uint64_t kk = cost_key(cst[j]);
+        if (kk < best_k) {
+          best_k = kk;
+          best_i = c0 + j;
+        }
+      }
+    }
+  }
+  block_argmin(best_k, best_i);
+  if (threadIdx.x == 0) part[blockIdx.x - 1] = Rec{best_k, best_i};
 }
 
 }  // namespace mpc

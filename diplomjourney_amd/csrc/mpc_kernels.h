@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/mpc_rollout.h"
 #include "mpc_device.h"
 
@@ -83,20 +85,14 @@ __device__ __forceinline__ void block_argmin(uint64_t& k, int64_t& i) {
 }
 
 // Rollout of CPL adjacent candidates starting at column c0; costs in cst.
-template <int CPL, int INTEG, bool ROT, bool STATES, bool PL2>
+template <int CPL, int INTEG, int ROT, bool STATES, bool PL2>
 __device__ __forceinline__ void rollout_lane_l(const Consts& K, const double* __restrict__ v,
                                              const double* __restrict__ b, int64_t ld, int64_t c0,
                                              int n_steps, double (&cst)[CPL],
                                              double* __restrict__ states, int64_t n_cand) {
   double x[CPL], y[CPL], ph[CPL], sn[CPL], cs[CPL];
 #pragma unroll
-  for (int j = 0; j < CPL; ++j) {
-    x[j] = K.x;
-    y[j] = K.y;
-    ph[j] = K.phi;
-    sn[j] = K.s0;
-    cs[j] = K.c0;
-  }
+  for (int j = 0; j < CPL; ++j) step_start<ROT>(K, x[j], y[j], ph[j], sn[j], cs[j]);
   // Controls of step sr for this lane's CPL candidates: 16 B per lane per
   // array on the wide path (one 1 KiB wave-instruction each).
   auto load = [&](int sr, double (&vv)[CPL], double (&bb)[CPL]) {
@@ -136,8 +132,10 @@ __device__ __forceinline__ void rollout_lane_l(const Consts& K, const double* __
 #endif
       step_core<INTEG, ROT, PL2>(x[j], y[j], ph[j], sn[j], cs[j], vv[j], bb[j], K, bad[j]);
       if constexpr (STATES) {
-        states[(sr * 3 + 0) * n_cand + c0 + j] = x[j];
-        states[(sr * 3 + 1) * n_cand + c0 + j] = y[j];
+        double px = x[j], py = y[j];
+        if constexpr (ROT == kRotCum) cum_pose(K, x[j], y[j], px, py);
+        states[(sr * 3 + 0) * n_cand + c0 + j] = px;
+        states[(sr * 3 + 1) * n_cand + c0 + j] = py;
         states[(sr * 3 + 2) * n_cand + c0 + j] = ph[j];
       }
     }
@@ -168,6 +166,9 @@ __device__ __forceinline__ void rollout_lane_l(const Consts& K, const double* __
   // arguments; kept out of the loop so the loop carries no fallback code.
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
+    if constexpr (ROT == kRotCum) {
+      if (!bad[j]) cum_pose(K, x[j], y[j], x[j], y[j]);
+    }
     if (bad[j]) {
       x[j] = K.x;
       y[j] = K.y;
@@ -277,10 +278,22 @@ __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
 }
 
-template <int INTEG, bool ROT, bool PL2>
-__device__ __forceinline__ void rollout_lane_glds(const Consts& K, const double* __restrict__ v,
-                                                  const double* __restrict__ b, int64_t ld,
-                                                  int64_t c0, int n_steps, double (&cst)[2]) {
+struct NoPre {
+  __device__ void operator()() const {}
+};
+
+// pre(): called before K is first read (the chained episode step waits there
+// for this step's constants): ROT 0 / 1 once the first ring slots are in
+// flight; kRotCum only after the loop, which reads Kloop (the step size h and
+// the wheelbase terms; = K except in the chained step, which speculates them
+// in pre0(), called once the first ring slots are in flight).
+template <int INTEG, int ROT, bool PL2, class Pre = NoPre, class Pre0 = NoPre>
+__device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Consts& Kloop,
+                                                    const double* __restrict__ v,
+                                                    const double* __restrict__ b, int64_t ld,
+                                                    int64_t c0, int n_steps, double (&cst)[2],
+                                                    const Pre& pre = Pre{},
+                                                    const Pre0& pre0 = Pre0{}) {
   constexpr int CPL = 2;
   constexpr int R = kRing;
   const int lane = threadIdx.x & 63;
@@ -288,21 +301,21 @@ __device__ __forceinline__ void rollout_lane_glds(const Consts& K, const double*
   const uint32_t ring0 = __builtin_amdgcn_readfirstlane(lds_addr(&g_ring[wv][0][0][0]));
   constexpr uint32_t kSlot = 2 * 64 * sizeof(double2);  // 2 KiB
   auto dst = [&](int slot) { return ring0 + slot * kSlot; };
-  double x[CPL], y[CPL], ph[CPL], sn[CPL], cs[CPL];
-  bool bad[CPL];
-#pragma unroll
-  for (int j = 0; j < CPL; ++j) {
-    x[j] = K.x;
-    y[j] = K.y;
-    ph[j] = K.phi;
-    sn[j] = K.s0;
-    cs[j] = K.c0;
-    bad[j] = false;
-  }
 #pragma unroll
   for (int u = 0; u < R - 1; ++u)
     if (u < n_steps && MPC_EXPERIMENT != 2)
       glds_pair(v + u * ld + c0, b + u * ld + c0, dst(u), dst(u) + kSlot / 2);
+  if constexpr (ROT != kRotCum)
+    pre();
+  else
+    pre0();   // kRotCum: the loop constants Kloop (the chained step reads them here)
+  double x[CPL], y[CPL], ph[CPL], sn[CPL], cs[CPL];
+  bool bad[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    step_start<ROT>(Kloop, x[j], y[j], ph[j], sn[j], cs[j]);
+    bad[j] = false;
+  }
   double2 v2 = make_double2(0.0, 0.0), b2 = v2;   // the last slot's contents as read
   // leading trig coefficients pinned in VGPRs (opaque to the compiler, so not
   // re-materialised per step)
@@ -336,14 +349,31 @@ __device__ __forceinline__ void rollout_lane_glds(const Consts& K, const double*
         // the heading itself is not needed here (rotation mode carries sin/cos;
         // an irregular candidate is recomputed from K.phi), so no phi chain
         double ph0 = ROT ? 0.0 : ph[0], ph1 = ROT ? 0.0 : ph[1];
-        step_core<INTEG, ROT, PL2>(x[0], y[0], ph0, sn[0], cs[0], v2.x, b2.x, K, bad[0], &lead);
-        step_core<INTEG, ROT, PL2>(x[1], y[1], ph1, sn[1], cs[1], v2.y, b2.y, K, bad[1], &lead);
+        step_core<INTEG, ROT, PL2>(x[0], y[0], ph0, sn[0], cs[0], v2.x, b2.x, Kloop, bad[0],
+                                   &lead);
+        step_core<INTEG, ROT, PL2>(x[1], y[1], ph1, sn[1], cs[1], v2.y, b2.y, Kloop, bad[1],
+                                   &lead);
         if (!ROT) {
           ph[0] = ph0;
           ph[1] = ph1;
         }
       }
     }
+  }
+  if constexpr (ROT == kRotCum) {
+    // the start pose is first needed here (chained step: this step's
+    // constants are waited for now; if the step size speculated for the loop
+    // turns out different — an episode restart reset t — the lane recomputes)
+    pre();
+    if constexpr (!std::is_same_v<Pre, NoPre>) {
+      if (Kloop.h != K.h) {
+        rollout_lane_glds_k<INTEG, ROT, PL2>(K, K, v, b, ld, c0, n_steps, cst);
+        return;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CPL; ++j)
+      if (!bad[j]) cum_pose(K, x[j], y[j], x[j], y[j]);
   }
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
@@ -358,8 +388,15 @@ __device__ __forceinline__ void rollout_lane_glds(const Consts& K, const double*
   }
 }
 
+template <int INTEG, int ROT, bool PL2>
+__device__ __forceinline__ void rollout_lane_glds(const Consts& K, const double* __restrict__ v,
+                                                  const double* __restrict__ b, int64_t ld,
+                                                  int64_t c0, int n_steps, double (&cst)[2]) {
+  rollout_lane_glds_k<INTEG, ROT, PL2>(K, K, v, b, ld, c0, n_steps, cst);
+}
+
 // L a power of two or not: one loop body each (see step_core).
-template <int CPL, int INTEG, bool ROT, bool STATES>
+template <int CPL, int INTEG, int ROT, bool STATES>
 __device__ __forceinline__ void rollout_lane(const Consts& K, const double* __restrict__ v,
                                              const double* __restrict__ b, int64_t ld, int64_t c0,
                                              int n_steps, double (&cst)[CPL],
@@ -379,7 +416,7 @@ __device__ __forceinline__ void rollout_lane(const Consts& K, const double* __re
     rollout_lane_l<CPL, INTEG, ROT, STATES, false>(K, v, b, ld, c0, n_steps, cst, states, n_cand);
 }
 
-template <int CPL, int INTEG, bool ROT, bool STATES, bool KDEV>
+template <int CPL, int INTEG, int ROT, bool STATES, bool KDEV>
 __device__ __forceinline__ void rollout_argmin_body(
     const Consts& Karg, const Consts* __restrict__ Kdev, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part,
@@ -408,7 +445,7 @@ __device__ __forceinline__ void rollout_argmin_body(
 }
 
 // Scalar (CPL = 1), CoordinateTree-states and register-ring paths.
-template <int CPL, int INTEG, bool ROT, bool STATES, bool KDEV>
+template <int CPL, int INTEG, int ROT, bool STATES, bool KDEV>
 __global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(
     Consts Karg, const Consts* __restrict__ Kdev, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part,
@@ -424,7 +461,7 @@ __global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(
 #ifndef MPC_STREAM_WAVES
 #define MPC_STREAM_WAVES 5
 #endif
-template <int INTEG, bool ROT, bool KDEV>
+template <int INTEG, int ROT, bool KDEV>
 __global__ __launch_bounds__(kBlock, MPC_STREAM_WAVES) void k_rollout_argmin_stream(
     Consts Karg, const Consts* __restrict__ Kdev, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part) {
@@ -451,7 +488,7 @@ struct Winner {
 // x and y.  The winner is regular or irregular exactly as in rollout_lane
 // (same tests), and each branch repeats that path's operations in the same
 // order, so the emitted states are bitwise those the arg-min scored.
-template <int INTEG, bool ROT>
+template <int INTEG, int ROT>
 __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
                             const double* __restrict__ b, int64_t ld, int n_steps, uint64_t key,
                             int64_t col, int64_t reported_index, double incumbent,
@@ -553,7 +590,11 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
     win->v = s_v[0];
     win->beta = s_b0;
   }
-  double x = K.x, y = K.y, sn = K.s0, cs = K.c0, ph = K.phi;
+  double x, y, sn, cs, ph;
+  if (fast)
+    step_start<ROT>(K, x, y, ph, sn, cs);    // kRotCum: identity rotation, empty sums
+  else
+    step_start<0>(K, x, y, ph, sn, cs);
   for (int st = 0; st < n_steps; ++st) {
     if (fast) {
       ph = ph + s_dphi[st];
@@ -565,12 +606,14 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
     }
     x = position_step<INTEG>(x, s_v[st], cs, K);
     y = position_step<INTEG>(y, s_v[st], sn, K);
-    out->traj[st][0] = x;
-    out->traj[st][1] = y;
+    double px = x, py = y;
+    if (ROT == kRotCum && fast) cum_pose(K, x, y, px, py);
+    out->traj[st][0] = px;
+    out->traj[st][1] = py;
     out->traj[st][2] = ph;
     if (win && st < 3) {
-      win->tr[st][0] = x;
-      win->tr[st][1] = y;
+      win->tr[st][0] = px;
+      win->tr[st][1] = py;
       win->tr[st][2] = ph;
     }
   }
@@ -594,6 +637,8 @@ struct EpisodeHook {  // single-GPU episode: finalize also advances it
   EpisodeHead* H;     // nullptr: no hook
   mpc_episode_log_t* log;
   int cap;
+  uint64_t* chain_pub = nullptr;   // cleared with the update (ends a chain of chained steps)
+  int chain_pub_words = 0;
 };
 __device__ void episode_hook(const mpc_episode_config_t& c, const EpisodeHook& h,
                              const Winner& r, EpisodeHead& H);
@@ -624,7 +669,7 @@ __device__ __forceinline__ void load8_rec_sc1(const Rec* const (&p)[8], u64x2 (&
       : "memory");
 }
 
-template <int INTEG, bool ROT, bool KDEV, int NT, bool SC1>
+template <int INTEG, int ROT, bool KDEV, int NT, bool SC1>
 __device__ __forceinline__ void finalize_block(
     const Rec* __restrict__ part, int n_part, const Consts& K, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, int64_t index_base,
@@ -708,6 +753,7 @@ __device__ __forceinline__ void finalize_block(
     __builtin_memcpy(&H, s_head, sizeof(EpisodeHead));
     episode_hook(ecfg, hook, w, H);
     *hook.H = H;
+    for (int q = 0; q < hook.chain_pub_words; ++q) hook.chain_pub[q] = 0ull;
   }
 #ifdef MPC_FIN_TRACE
   if (threadIdx.x == 0) {   // debug builds only: 10-ns ticks in unused trajectory slots
@@ -719,7 +765,7 @@ __device__ __forceinline__ void finalize_block(
 #endif
 }
 
-template <int INTEG, bool ROT, bool KDEV>
+template <int INTEG, int ROT, bool KDEV>
 __global__ __launch_bounds__(kFinBlock) void k_finalize(
     const Rec* __restrict__ part, int n_part, Consts Karg, const Consts* __restrict__ Kdev,
     const double* __restrict__ v, const double* __restrict__ b, int64_t n_cand, int n_steps,
@@ -739,7 +785,7 @@ __global__ __launch_bounds__(kFinBlock) void k_finalize(
 // to the launch counter (agent-scope atomic); the block whose add returns
 // gridDim-1 is last, and its threads read every record `sc1` after a
 // workgroup barrier.  The last block re-arms the counter for the next launch.
-template <int CPL, int INTEG, bool ROT>
+template <int CPL, int INTEG, int ROT>
 __global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_episode(
     const Consts* __restrict__ Kdev, const double* __restrict__ v, const double* __restrict__ b,
     int64_t n_cand, int n_steps, int64_t index_base, Rec* __restrict__ part,
@@ -814,7 +860,7 @@ __device__ __forceinline__ Consts consts_from_problem(const mpc_problem_t& p) {
 }
 
 // --------------------------- batched robots --------------------------------
-template <int CPL, int INTEG, bool ROT>
+template <int CPL, int INTEG, int ROT>
 __global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin_batched(
     const mpc_problem_t* __restrict__ probs, const double* __restrict__ v,
     const double* __restrict__ b, int64_t cand, int n_steps, int64_t ld, Rec* __restrict__ part) {
@@ -843,7 +889,7 @@ __global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin_batche
     part[static_cast<int64_t>(r) * gridDim.x + blockIdx.x] = Rec{best_k, best_i};
 }
 
-template <int INTEG, bool ROT>
+template <int INTEG, int ROT>
 __global__ __launch_bounds__(kBlock) void k_finalize_batched(
     const Rec* __restrict__ part, int n_part, const mpc_problem_t* __restrict__ probs,
     const double* __restrict__ incumbents, const double* __restrict__ v,

@@ -82,15 +82,38 @@ using IC = std::integral_constant<int, V>;
 template <bool V>
 using BC = std::integral_constant<bool, V>;
 
-// integrator = MPC_INTEG_* [| MPC_HEADING_ROTATE]  ->  f(IC<INTEG>, BC<ROT>)
-int mode_ok(int32_t integrator) {
-  if (integrator & ~(0xff | MPC_HEADING_ROTATE)) return MPC_ERR_UNSUPPORTED;
+// integrator = MPC_INTEG_* [| MPC_HEADING_ROTATE | MPC_HEADING_CUMULATIVE]
+//   -> f(IC<INTEG>, IC<ROT>), ROT 0 direct heading, 1 rotation, 2 (kRotCum)
+//   rotation from the identity with the pose applied last (rect only).
+// allow_cum = false for the full-tree entry points (their own recurrence).
+int mode_ok(int32_t integrator, bool allow_cum = true) {
+  if (integrator & ~(0xff | MPC_HEADING_ROTATE | MPC_HEADING_CUMULATIVE))
+    return MPC_ERR_UNSUPPORTED;
   const int integ = integrator & 0xff;
-  return (integ == MPC_INTEG_QK21 || integ == MPC_INTEG_RECT) ? MPC_OK : MPC_ERR_UNSUPPORTED;
+  if (integ != MPC_INTEG_QK21 && integ != MPC_INTEG_RECT) return MPC_ERR_UNSUPPORTED;
+  if ((integrator & MPC_HEADING_CUMULATIVE) && (!allow_cum || integ != MPC_INTEG_RECT))
+    return MPC_ERR_UNSUPPORTED;
+  return MPC_OK;
 }
+
+inline bool is_cum(int32_t integrator) { return (integrator & MPC_HEADING_CUMULATIVE) != 0; }
 
 template <class F>
 void dispatch_mode(int32_t integrator, F&& f) {
+  const bool rot = (integrator & MPC_HEADING_ROTATE) != 0;
+  if ((integrator & 0xff) == MPC_INTEG_RECT) {
+    if (is_cum(integrator)) f(IC<MPC_INTEG_RECT>{}, IC<kRotCum>{});
+    else if (rot) f(IC<MPC_INTEG_RECT>{}, IC<1>{});
+    else f(IC<MPC_INTEG_RECT>{}, IC<0>{});
+  } else {
+    if (rot) f(IC<MPC_INTEG_QK21>{}, IC<1>{});
+    else f(IC<MPC_INTEG_QK21>{}, IC<0>{});
+  }
+}
+
+// The full-tree kernels: direct or rotation heading only.
+template <class F>
+void dispatch_mode2(int32_t integrator, F&& f) {
   const bool rot = (integrator & MPC_HEADING_ROTATE) != 0;
   if ((integrator & 0xff) == MPC_INTEG_RECT) {
     if (rot) f(IC<MPC_INTEG_RECT>{}, BC<true>{});
@@ -105,7 +128,7 @@ void dispatch_mode(int32_t integrator, F&& f) {
 // per instantiation and device.  The fused launch is sized to ONE resident
 // round: each block's end-of-launch hand-off (sc1 store + counter atomic) is
 // then paid once per block, not once per tile round.
-template <int CPL, int I, bool R>
+template <int CPL, int I, int R>
 int64_t fused_grid(int64_t n_cand) {
   static int64_t cache[16] = {0};
   int dev = 0;
@@ -140,7 +163,7 @@ void launch_rollout(hipStream_t st, int32_t integrator, const Consts& K, const C
   const bool wide = wide_ok(v, b, n_cand);
   dispatch_mode(integrator, [&](auto integ, auto rot) {
     constexpr int I = decltype(integ)::value;
-    constexpr bool R = decltype(rot)::value;
+    constexpr int R = decltype(rot)::value;
     if (wide)
       k_rollout_argmin_stream<I, R, KDEV><<<rollout_grid<kCplWide>(n_cand), kBlock, 0, st>>>(
           K, Kdev, v, b, n_cand, n_steps, part);
@@ -159,7 +182,7 @@ void launch_finalize(hipStream_t st, int32_t integrator, const Rec* part, int n_
                      const mpc_episode_config_t& ecfg, const EpisodeHook& hook) {
   dispatch_mode(integrator, [&](auto integ, auto rot) {
     constexpr int I = decltype(integ)::value;
-    constexpr bool R = decltype(rot)::value;
+    constexpr int R = decltype(rot)::value;
     k_finalize<I, R, KDEV><<<1, kFinBlock, 0, st>>>(part, n_part, K, Kdev, v, b, n_cand, n_steps,
                                                     index_base, incumbent, incumbent_dev, out,
                                                     ecfg, hook);
@@ -222,7 +245,7 @@ int mpc_rollout_partials(const mpc_problem_t* p, const double* v_sc, const doubl
     // CoordinateTree materialisation path: one candidate per lane, all states out.
     dispatch_mode(integrator, [&](auto integ, auto rot) {
       constexpr int I = decltype(integ)::value;
-      constexpr bool R = decltype(rot)::value;
+      constexpr int R = decltype(rot)::value;
       k_rollout_argmin<1, I, R, true, false>
           <<<rollout_grid<1>(n_cand), kBlock, 0, st>>>(
               K, nullptr, v_sc, beta_sc, n_cand, n_steps, part, states_out);
@@ -287,7 +310,7 @@ int mpc_rollout_argmin_batched(const mpc_problem_t* problems, const double* incu
   Rec* part = static_cast<Rec*>(ws);
   dispatch_mode(integrator, [&](auto integ, auto rot) {
     constexpr int I = decltype(integ)::value;
-    constexpr bool R = decltype(rot)::value;
+    constexpr int R = decltype(rot)::value;
     if (wide)
       k_rollout_argmin_batched<kCplWide, I, R>
           <<<grid, kBlock, 0, st>>>(problems, v_sc, beta_sc, cand_per_problem, n_steps, ld, part);
@@ -298,7 +321,7 @@ int mpc_rollout_argmin_batched(const mpc_problem_t* problems, const double* incu
   if (last_hip_status() != MPC_OK) return MPC_ERR_HIP;
   dispatch_mode(integrator, [&](auto integ, auto rot) {
     constexpr int I = decltype(integ)::value;
-    constexpr bool R = decltype(rot)::value;
+    constexpr int R = decltype(rot)::value;
     k_finalize_batched<I, R><<<n_problems, kBlock, 0, st>>>(
         part, static_cast<int>(per_robot), problems, incumbents, v_sc, beta_sc, cand_per_problem,
         n_steps, ld, out);
@@ -386,7 +409,8 @@ int mpc_episode_finalize(void* state, const double* v_sc, const double* beta_sc,
   EpisodeState* S = static_cast<EpisodeState*>(state);
   const int n_part = static_cast<int>(partial_count(v_sc, beta_sc, n_cand, false));
   const mpc_episode_config_t ecfg = advance ? *advance : mpc_episode_config_t{};
-  const EpisodeHook hook{advance ? &S->h : nullptr, log, log_capacity};
+  const EpisodeHook hook{advance ? &S->h : nullptr, log, log_capacity,
+                         advance ? S->chain_pub : nullptr, advance ? kPubWords : 0};
   launch_finalize<true>(reinterpret_cast<hipStream_t>(stream), integrator,
                         static_cast<const Rec*>(ws), n_part, Consts{}, &S->h.K, v_sc, beta_sc,
                         n_cand, n_steps, index_base, 0.0, &S->h.incumbent, out, ecfg, hook);
@@ -405,12 +429,13 @@ int mpc_episode_rollout(void* state, const double* v_sc, const double* beta_sc, 
   if (advance && (check_episode_cfg(advance) != MPC_OK || log_capacity < 0)) return MPC_ERR_ARG;
   EpisodeState* S = static_cast<EpisodeState*>(state);
   const mpc_episode_config_t ecfg = advance ? *advance : mpc_episode_config_t{};
-  const EpisodeHook hook{advance ? &S->h : nullptr, log, log_capacity};
+  const EpisodeHook hook{advance ? &S->h : nullptr, log, log_capacity,
+                         advance ? S->chain_pub : nullptr, advance ? kPubWords : 0};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const bool wide = wide_ok(v_sc, beta_sc, n_cand);
   dispatch_mode(integrator, [&](auto integ, auto rot) {
     constexpr int I = decltype(integ)::value;
-    constexpr bool R = decltype(rot)::value;
+    constexpr int R = decltype(rot)::value;
     if (wide)
       k_rollout_episode<kCplWide, I, R><<<fused_grid<kCplWide, I, R>(n_cand), kBlock, 0, st>>>(
           &S->h.K, v_sc, beta_sc, n_cand, n_steps, index_base, static_cast<Rec*>(ws), &S->done,
@@ -421,6 +446,62 @@ int mpc_episode_rollout(void* state, const double* v_sc, const double* beta_sc, 
           &S->h.incumbent, out, ecfg, hook);
   });
   return last_hip_status();
+}
+
+int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t mode,
+                           uint32_t epoch, const double* v_sc, const double* beta_sc,
+                           int64_t n_cand,
+                           int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
+                           const void* ws_prev, size_t ws_bytes, const double* v_prev,
+                           const double* beta_prev, mpc_result_t* out_prev,
+                           const mpc_result_t* gathered, int32_t n_gathered,
+                           mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream) {
+  if (check_episode_cfg(cfg) != MPC_OK ||
+      check_episode_arrays(state, v_sc, beta_sc, n_cand, n_steps) != MPC_OK || index_base < 0 ||
+      log_capacity < 0 || (mode != MPC_CHAIN_FINALIZE && mode != MPC_CHAIN_ADVANCE) || epoch == 0)
+    return MPC_ERR_ARG;
+  if (mode_ok(integrator) != MPC_OK || !is_cum(integrator) || !wide_ok(v_sc, beta_sc, n_cand))
+    return MPC_ERR_UNSUPPORTED;
+  if (!ws || ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
+  int has_prev = 0;
+  if (mode == MPC_CHAIN_FINALIZE && v_prev) {
+    if (!beta_prev || !out_prev || !ws_prev || !wide_ok(v_prev, beta_prev, n_cand))
+      return MPC_ERR_ARG;
+    has_prev = 1;
+  }
+  if (mode == MPC_CHAIN_ADVANCE && gathered) {
+    if (n_gathered < 1) return MPC_ERR_ARG;
+    has_prev = 1;
+  }
+  EpisodeState* S = static_cast<EpisodeState*>(state);
+  int e;
+  const int pl2 = frexp(cfg->L, &e) == 0.5 ? 1 : 0;   // as consts_from_problem decides
+  const int64_t grid = rollout_grid<kCplWide>(n_cand) + 1;
+  const int n_part_prev = static_cast<int>(rollout_grid<kCplWide>(n_cand));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  constexpr int I = MPC_INTEG_RECT;
+  if (mode == MPC_CHAIN_FINALIZE)
+    k_episode_chain<I, kRotCum, kChainFin><<<grid, kBlock, 0, st>>>(
+        S, epoch, v_sc, beta_sc, n_cand, n_steps, pl2, static_cast<Rec*>(ws), has_prev,
+        static_cast<const Rec*>(ws_prev), n_part_prev, v_prev, beta_prev, index_base, out_prev,
+        nullptr, 0, *cfg, log, log_capacity);
+  else
+    k_episode_chain<I, kRotCum, kChainAdv><<<grid, kBlock, 0, st>>>(
+        S, epoch, v_sc, beta_sc, n_cand, n_steps, pl2, static_cast<Rec*>(ws), has_prev, nullptr,
+        0, nullptr, nullptr, index_base, nullptr, gathered, n_gathered, *cfg, log, log_capacity);
+  return last_hip_status();
+}
+
+int mpc_episode_chain_error(const void* state, int32_t* error, mpc_stream_t stream) {
+  if (!state || !error) return MPC_ERR_ARG;
+  uint32_t e = 0;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemcpyAsync(&e, &static_cast<const EpisodeState*>(state)->chain_error, sizeof(e),
+                     hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return MPC_ERR_HIP;
+  *error = static_cast<int32_t>(e);
+  return MPC_OK;
 }
 
 int mpc_episode_expand(const mpc_episode_config_t* cfg, void* state, double* v_sc,
@@ -464,7 +545,7 @@ int mpc_fulltree_argmin(const mpc_fulltree_problem_t* p, const double* v_grid, i
   if (n_shards < 1 || shard < 0 || shard >= n_shards) return MPC_ERR_ARG;
   const int64_t s1 = static_cast<int64_t>(n_v) * n_beta;
   if (s1 > 2000000) return MPC_ERR_ARG;  // S1^3 must fit int64 leaf indices
-  if (mode_ok(integrator) != MPC_OK) return MPC_ERR_UNSUPPORTED;
+  if (mode_ok(integrator, false) != MPC_OK) return MPC_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < mpc_fulltree_workspace_bytes(n_v, n_beta)) return MPC_ERR_WORKSPACE;
   mpc_problem_t q;
   q.x = p->x;
@@ -490,7 +571,7 @@ int mpc_fulltree_argmin(const mpc_fulltree_problem_t* p, const double* v_grid, i
   const int64_t item_hi = item_lo + base + (shard < rem ? 1 : 0);
   const int64_t grid =
       std::max<int64_t>(1, std::min(cdiv(item_hi - item_lo, kWaves), kFtMaxBlocks));
-  dispatch_mode(integrator, [&](auto integ, auto rot) {
+  dispatch_mode2(integrator, [&](auto integ, auto rot) {
     constexpr int I = decltype(integ)::value;
     constexpr bool R = decltype(rot)::value;
     k_ft_controls<I><<<cdiv(s1, kBlock), kBlock, 0, st>>>(K, v_grid, beta_grid, n_beta, s1, ctl,
@@ -528,7 +609,7 @@ int mpc_fulltree_argmin_batched(const mpc_fulltree_problem_t* problems,
     return MPC_ERR_ARG;
   const int64_t s1 = static_cast<int64_t>(n_v) * n_beta;
   if (s1 > 2000000) return MPC_ERR_ARG;
-  if (mode_ok(integrator) != MPC_OK) return MPC_ERR_UNSUPPORTED;
+  if (mode_ok(integrator, false) != MPC_OK) return MPC_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < mpc_fulltree_batched_workspace_bytes(n_problems, n_v, n_beta))
     return MPC_ERR_WORKSPACE;
   mpc_problem_t q = {};
@@ -548,7 +629,7 @@ int mpc_fulltree_argmin_batched(const mpc_fulltree_problem_t* problems,
   if (hipMemsetAsync(no_rot, 0, sizeof(uint32_t), st) != hipSuccess) return MPC_ERR_HIP;
   const int64_t bx = ft_blocks_per_robot(s1, n_problems);
   k_ft_robots<<<cdiv(n_problems, 256), 256, 0, st>>>(problems, n_problems, L, t_a, t_b, robots);
-  dispatch_mode(integrator, [&](auto integ, auto rot) {
+  dispatch_mode2(integrator, [&](auto integ, auto rot) {
     constexpr int I = decltype(integ)::value;
     constexpr bool R = decltype(rot)::value;
     k_ft_controls<I><<<cdiv(s1, kBlock), kBlock, 0, st>>>(Kw, v_grid, beta_grid, n_beta, s1,

@@ -178,7 +178,7 @@ class DeviceEpisode:
 
     def __init__(self, engine, n_cand_total, n_steps, rank=0, world=1, seed=20261015,
                  integrator="rect", group=None, start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3),
-                 log_capacity=4096, split=True, exchange=None):
+                 log_capacity=4096, split=True, exchange=None, chain=False):
         self.eng = engine
         self.lib = native.lib()
         self.n_total = int(n_cand_total)
@@ -209,6 +209,13 @@ class DeviceEpisode:
         self.exchange = world > 1 if exchange is None else bool(exchange)
         if world > 1 and not self.exchange:
             raise ValueError("world > 1 needs the exchange step")
+        # chain: each step's launch also completes the previous step
+        # (mpc_episode_chain_step; caller-resident controls, aligned path);
+        # flush() completes the last one.
+        self.chain = bool(chain)
+        self._ws = [self.ws, torch.empty_like(self.ws)] if self.chain else [self.ws]
+        self._pending = None
+        self._epoch = 0
         self.steps_enqueued = 0
         self.reset()
 
@@ -219,6 +226,86 @@ class DeviceEpisode:
         native.check(self.lib.mpc_episode_reset(ctypes.byref(self.cfg), self.state.data_ptr(),
                                                 self._stream()), "mpc_episode_reset")
         self.steps_enqueued = 0
+        self._pending = None
+
+    def _check_controls(self, controls):
+        v, b = controls
+        if (tuple(v.shape) != (self.n_steps, self.n_local) or v.shape != b.shape
+                or v.dtype != torch.float64 or b.dtype != torch.float64
+                or not v.is_contiguous() or not b.is_contiguous()
+                or v.device != self.v_sc.device or b.device != self.v_sc.device):
+            raise ValueError("controls must be contiguous float64 [n_steps, n_local] "
+                             "tensors on the episode's device")
+        return v, b
+
+    def _chain_step(self, controls, events=None):
+        """One chained launch: this step's rollout + the previous step's
+        completion (one GPU: finalize + update; multi-GPU: selection over the
+        gathered winners + update), then on multi-GPU this step's local
+        finalize and the all_gather."""
+        L, st = self.lib, self._stream()
+        v, b = self._check_controls(controls)
+        self.cur = (v, b)
+        ws, ws_prev = self._ws[0], self._ws[1]
+        pend = self._pending
+        if events:
+            events[0].record()
+        if not self.exchange:
+            pv, pb = (pend[0].data_ptr(), pend[1].data_ptr()) if pend else (None, None)
+            native.check(L.mpc_episode_chain_step(
+                ctypes.byref(self.cfg), self.state.data_ptr(), 1, self._next_epoch(),
+                v.data_ptr(), b.data_ptr(),
+                self.n_local, self.n_steps, self.lo, self._integ, ws.data_ptr(),
+                ws_prev.data_ptr(), ws.numel(), pv, pb, self.local.data_ptr(), None, 0,
+                self.log.data_ptr(), self.log_capacity, st), "mpc_episode_chain_step")
+            self._pending = (v, b)
+        else:
+            native.check(L.mpc_episode_chain_step(
+                ctypes.byref(self.cfg), self.state.data_ptr(), 2, self._next_epoch(),
+                v.data_ptr(), b.data_ptr(),
+                self.n_local, self.n_steps, self.lo, self._integ, ws.data_ptr(),
+                ws_prev.data_ptr(), ws.numel(), None, None, None,
+                pend.data_ptr() if pend is not None else None, self.world if pend is not None
+                else 0, self.log.data_ptr(), self.log_capacity, st), "mpc_episode_chain_step")
+            native.check(L.mpc_episode_finalize(
+                self.state.data_ptr(), v.data_ptr(), b.data_ptr(), self.n_local, self.n_steps,
+                self.lo, self._integ, ws.data_ptr(), ws.numel(), self.local.data_ptr(), None,
+                None, 0, st), "mpc_episode_finalize")
+            self._pending = gather_results(self.local, self.group)
+        if events:
+            events[1].record()
+        if pend is not None:
+            self.steps_enqueued += 1
+        self._ws.reverse()
+
+    def _next_epoch(self):
+        self._epoch = self._epoch % 0xFFFFFFFF + 1      # nonzero, differs from the last
+        return self._epoch
+
+    def flush(self):
+        """Complete the step a chained launch left pending (no-op otherwise)."""
+        pend, self._pending = self._pending, None
+        if pend is None:
+            return
+        L, st = self.lib, self._stream()
+        if not self.exchange:
+            v, b = pend
+            native.check(L.mpc_episode_finalize(
+                self.state.data_ptr(), v.data_ptr(), b.data_ptr(), self.n_local, self.n_steps,
+                self.lo, self._integ, self._ws[1].data_ptr(), self._ws[1].numel(),
+                self.local.data_ptr(), ctypes.byref(self.cfg), self.log.data_ptr(),
+                self.log_capacity, st), "mpc_episode_finalize")
+        else:
+            native.check(L.mpc_episode_advance(
+                ctypes.byref(self.cfg), self.state.data_ptr(), pend.data_ptr(), self.world,
+                self.log.data_ptr(), self.log_capacity, st), "mpc_episode_advance")
+        self.steps_enqueued += 1
+
+    def chain_error(self):
+        e = ctypes.c_int32(0)
+        native.check(self.lib.mpc_episode_chain_error(self.state.data_ptr(), ctypes.byref(e),
+                                                      self._stream()), "mpc_episode_chain_error")
+        return int(e.value)
 
     def expand(self, events=None, controls=None):
         """Grid + sampler + rollout + finalize for this rank's shard.
@@ -229,6 +316,7 @@ class DeviceEpisode:
         the rollout (+ selection) launch."""
         st = self._stream()
         L = self.lib
+        self.flush()
         if controls is None:
             native.check(L.mpc_episode_sample(ctypes.byref(self.cfg), self.state.data_ptr(),
                                               self.v_sc.data_ptr(), self.b_sc.data_ptr(),
@@ -236,14 +324,7 @@ class DeviceEpisode:
                          "mpc_episode_sample")
             self.cur = (self.v_sc, self.b_sc)
         else:
-            v, b = controls
-            if (tuple(v.shape) != (self.n_steps, self.n_local) or v.shape != b.shape
-                    or v.dtype != torch.float64 or b.dtype != torch.float64
-                    or not v.is_contiguous() or not b.is_contiguous()
-                    or v.device != self.v_sc.device or b.device != self.v_sc.device):
-                raise ValueError("controls must be contiguous float64 [n_steps, n_local] "
-                                 "tensors on the episode's device")
-            self.cur = (v, b)
+            self.cur = self._check_controls(controls)
         one_gpu = not self.exchange  # one GPU: the step's launch also advances the episode
         args = (self.state.data_ptr(), self.cur[0].data_ptr(), self.cur[1].data_ptr(),
                 self.n_local, self.n_steps, self.lo, self._integ, self.ws.data_ptr(),
@@ -268,6 +349,7 @@ class DeviceEpisode:
     def partials(self, st=None):
         """The streaming rollout/arg-min kernel alone on the current controls
         (writes only the workspace block records; the episode is unchanged)."""
+        self.flush()
         v, b = self.cur
         native.check(self.lib.mpc_episode_partials(
             self.state.data_ptr(), v.data_ptr(), b.data_ptr(), self.n_local,
@@ -287,10 +369,19 @@ class DeviceEpisode:
         self.steps_enqueued += 1
 
     def step(self, events=None, controls=None):
+        if self.chain and controls is not None and self._chainable(controls):
+            self._chain_step(controls, events)
+            return
         self.expand(events, controls)
         self.advance()
 
+    def _chainable(self, controls):
+        v, b = controls
+        return (self.integrator == "rect+cum" and self.n_local % 2 == 0
+                and v.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
+
     def read_log(self):
+        self.flush()
         torch.cuda.current_stream().synchronize()
         raw = self.log.cpu().numpy().tobytes()
         n = min(self.steps_enqueued, self.log_capacity)

@@ -55,6 +55,15 @@ enum { MPC_INTEG_QK21 = 0, MPC_INTEG_RECT = 1 };
  * candidate-step.  Candidates with an increment |dphi| > 0.2 (or |beta| > 1.1)
  * are recomputed with direct evaluation. */
 #define MPC_HEADING_ROTATE 0x100
+/* RECT only: the rotation recurrence started from the identity (sin, cos) =
+ * (0, 1) and position sums (A, B) = (0, 0) — A = sum v h cos(Phi_k),
+ * B = sum v h sin(Phi_k) over the heading increments Phi_k since the start —
+ * and the start pose applied last: x = x0 + (c0 A - s0 B), y = y0 + (s0 A +
+ * c0 B).  Same work per step as MPC_HEADING_ROTATE, other roundings (ulps);
+ * a candidate's rollout then needs no start pose, which lets a chained
+ * episode step (mpc_episode_chain_step) roll out step k while step k-1 is
+ * still being selected.  Irregular candidates as above. */
+#define MPC_HEADING_CUMULATIVE 0x200
 
 /* One MPC problem (one robot at one MPC step). */
 typedef struct mpc_problem {
@@ -215,6 +224,37 @@ int mpc_episode_finalize(void* state, const double* v_sc, const double* beta_sc,
                          int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
                          size_t ws_bytes, mpc_result_t* out, const mpc_episode_config_t* advance,
                          mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
+
+/* Chained step (integrator MPC_INTEG_RECT | MPC_HEADING_CUMULATIVE): ONE
+ * launch = the streaming rollout of this step (v_sc / beta_sc, records into
+ * ws) + the selection that completes the PREVIOUS step, run by the launch's
+ * first block while the other blocks roll out (they need its published
+ * constants only for the final pose transform and the criterion):
+ *   mode MPC_CHAIN_FINALIZE (one GPU): the previous step's records (ws_prev),
+ *        controls (v_prev / beta_prev; NULL = no previous step) -> winner re-
+ *        rolled into out_prev, episode update (cfg, log);
+ *   mode MPC_CHAIN_ADVANCE (multi-GPU): selection over the previous step's
+ *        gathered per-rank winners (gathered, n_gathered; NULL = none) and the
+ *        update; the local winner of THIS step still needs
+ *        mpc_episode_finalize (advance = NULL) before the all_gather.
+ * The last step of a chain is completed by mpc_episode_finalize (one GPU) or
+ * mpc_episode_advance (multi-GPU); either ends the chain.  epoch: nonzero,
+ * different from the previous chained launch's.  Aligned path only (n_cand
+ * even, 16-B aligned controls): MPC_ERR_UNSUPPORTED otherwise.  ws / ws_prev:
+ * two workspaces of mpc_workspace_bytes(n_cand, n_steps) each, alternated. */
+#define MPC_CHAIN_FINALIZE 1
+#define MPC_CHAIN_ADVANCE 2
+int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t mode,
+                           uint32_t epoch, const double* v_sc, const double* beta_sc,
+                           int64_t n_cand,
+                           int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
+                           const void* ws_prev, size_t ws_bytes, const double* v_prev,
+                           const double* beta_prev, mpc_result_t* out_prev,
+                           const mpc_result_t* gathered, int32_t n_gathered,
+                           mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
+/* Nonzero if a chained step's wait for its constants ever timed out (the
+ * launch then ran on stale constants); reads the device state (syncs). */
+int mpc_episode_chain_error(const void* state, int32_t* error, mpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Full-tree MPC of run_math_model.py / math_model.py.

@@ -30,16 +30,19 @@ extern "C" int replica_rollout(const mpc_problem_t* p, const double* v, const do
   K.s0 = sn(p->phi);
   K.c0 = cs(p->phi);
   const bool rot = (integ & MPC_HEADING_ROTATE) != 0;
+  const bool cum = (integ & MPC_HEADING_CUMULATIVE) != 0;
   const int ig = integ & 0xff;
   double traj[3 * MPC_MAX_STEPS];
   for (int64_t c = 0; c < n_cand; ++c) {
     double cst;
-    if (ig == MPC_INTEG_RECT)
-      cst = rot ? mpc::rollout_candidate<MPC_INTEG_RECT, true>(K, v, b, n_cand, c, n_steps, traj)
-                : mpc::rollout_candidate<MPC_INTEG_RECT, false>(K, v, b, n_cand, c, n_steps, traj);
+    if (ig == MPC_INTEG_RECT && cum)
+      cst = mpc::rollout_candidate<MPC_INTEG_RECT, mpc::kRotCum>(K, v, b, n_cand, c, n_steps, traj);
+    else if (ig == MPC_INTEG_RECT)
+      cst = rot ? mpc::rollout_candidate<MPC_INTEG_RECT, 1>(K, v, b, n_cand, c, n_steps, traj)
+                : mpc::rollout_candidate<MPC_INTEG_RECT, 0>(K, v, b, n_cand, c, n_steps, traj);
     else
-      cst = rot ? mpc::rollout_candidate<MPC_INTEG_QK21, true>(K, v, b, n_cand, c, n_steps, traj)
-                : mpc::rollout_candidate<MPC_INTEG_QK21, false>(K, v, b, n_cand, c, n_steps, traj);
+      cst = rot ? mpc::rollout_candidate<MPC_INTEG_QK21, 1>(K, v, b, n_cand, c, n_steps, traj)
+                : mpc::rollout_candidate<MPC_INTEG_QK21, 0>(K, v, b, n_cand, c, n_steps, traj);
     if (states)
       for (int s = 0; s < n_steps; ++s)
         for (int k = 0; k < 3; ++k) states[(s * 3 + k) * n_cand + c] = traj[3 * s + k];

@@ -392,3 +392,113 @@ def test_device_episode_exchange_path_and_graph_capture(engine):
     finally:
         if own:
             dist.destroy_process_group()
+
+
+def _episode_log(ep):
+    return [(r.step, r.index, r.cost, r.x, r.y, r.phi, r.v, r.beta, r.p, r.episode)
+            for r in ep.read_log()]
+
+
+@pytest.mark.parametrize("integ", ["rect+cum"])
+def test_chained_episode_matches_separate_launches(engine, integ):
+    """Chained steps (mpc_episode_chain_step: step k's rollout and step k-1's
+    finalize + episode update in ONE launch, the tile blocks waiting on device
+    for block 0's published constants) log exactly the steps of the
+    two-launch device episode over 130 steps of resident batches — operator
+    events at p = 60/90/110 included — eagerly and replayed from a HIP graph
+    whose last launch is the flush; a launch whose last tile is partial
+    (50_000 = 97 tiles of 512 + 336)."""
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.episode import DeviceEpisode
+    n, ns, steps = 50_000, 10, 130
+    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
+    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
+    pool = [engine.sample_controls(V, B, n, ns, 500 + i) for i in range(8)]
+    ref = DeviceEpisode(engine, n, ns, integrator=integ, log_capacity=256)
+    for i in range(steps):
+        ref.step(controls=pool[i % 8])
+    want = _episode_log(ref)
+    assert len(want) == steps and {r[8] for r in want} >= {60, 90, 110}
+    ch = DeviceEpisode(engine, n, ns, integrator=integ, log_capacity=256, chain=True)
+    half = steps // 2
+    for i in range(half):
+        ch.step(controls=pool[i % 8])
+    ch.flush()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    n0 = ch.steps_enqueued
+    with torch.cuda.graph(g):
+        for i in range(half, steps):
+            ch.step(controls=pool[i % 8])
+        ch.flush()
+    ch.steps_enqueued = n0
+    g.replay()
+    ch.steps_enqueued += steps - half
+    assert _episode_log(ch) == want
+    assert ch.chain_error() == 0
+
+
+def test_chained_episode_multi_tile_blocks(engine):
+    """Chained steps when blocks stride over several tiles (1.1e6 candidates
+    > 2048 blocks x 512) equal the two-launch episode."""
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.episode import DeviceEpisode
+    n, ns, steps = 1_100_000, 6, 5
+    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
+    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
+    pool = [engine.sample_controls(V, B, n, ns, 700 + i) for i in range(steps)]
+    ref = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=16)
+    ch = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=16, chain=True)
+    for i in range(steps):
+        ref.step(controls=pool[i])
+        ch.step(controls=pool[i])
+    assert _episode_log(ch) == _episode_log(ref)
+    assert ch.chain_error() == 0
+
+
+def test_chained_exchange_path_and_graph_capture(engine):
+    """The chained multi-GPU step (launch: rollout of step k + selection over
+    step k-1's gathered winners; then step k's local finalize and the RCCL
+    all_gather) over a 1-rank nccl group, eager and graph-captured, logs the
+    steps of the single-GPU episode."""
+    import torch.distributed as dist
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.episode import DeviceEpisode
+    n, ns, steps = 40_000, 10, 12
+    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
+    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
+    pool = [engine.sample_controls(V, B, n, ns, 900 + i) for i in range(steps)]
+    ref = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64)
+    for i in range(steps):
+        ref.step(controls=pool[i])
+    want = _episode_log(ref)
+    own = not dist.is_initialized()
+    if own:
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64,
+                           exchange=True, chain=True)
+        half = steps // 2
+        for i in range(half):
+            ep.step(controls=pool[i])
+        ep.flush()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        n0 = ep.steps_enqueued
+        with torch.cuda.graph(g):
+            for i in range(half, steps):
+                ep.step(controls=pool[i])
+            ep.flush()
+        ep.steps_enqueued = n0
+        g.replay()
+        ep.steps_enqueued += steps - half
+        assert _episode_log(ep) == want
+        assert ep.chain_error() == 0
+    finally:
+        if own:
+            dist.destroy_process_group()

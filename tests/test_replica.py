@@ -52,13 +52,15 @@ def test_replica_vs_oracle_synthetic(oracle):
     assert frac_equal > 0.5                 # most states bit-identical to the reference math
 
 
-def test_replica_rotation_mode_vs_oracle(oracle):
-    """Heading-rotation mode: a few ulp from the reference's direct sin/cos,
-    same arg-min."""
+@pytest.mark.parametrize("integ", ["rect+rot", "rect+cum"])
+def test_replica_rotation_mode_vs_oracle(oracle, integ):
+    """Heading-rotation modes (rotation of the pose's heading; rotation from
+    the identity with the pose applied last): a few ulp from the reference's
+    direct sin/cos, same arg-min."""
     from diplomjourney_amd.abi import make_problem
     v, b = _case(20_000, 12, 6)
     p = make_problem(0.2, -0.1, 2.9, 2, 3, 0.5, 0.5, 0.5, 0.35, 0.4)
-    st, costs = replica_rollout(p, v, b, "rect+rot")
+    st, costs = replica_rollout(p, v, b, integ)
     ref, rc, rs = oracle.rollout_argmin(p, v, b, integ="rect", want_costs=True, want_states=True)
     assert int(np.argmin(costs)) == ref.index
     assert np.abs(st - rs).max() <= 1e-13
@@ -68,7 +70,8 @@ def test_replica_rotation_mode_vs_oracle(oracle):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,ns,integ", [(100_000, 5, "rect"), (30_001, 12, "qk21"),
                                         (4096, 32, "rect"), (100_000, 10, "rect+rot"),
-                                        (30_001, 7, "qk21+rot")])
+                                        (30_001, 7, "qk21+rot"), (100_000, 10, "rect+cum"),
+                                        (30_001, 9, "rect+cum")])
 def test_gpu_bitwise_equals_replica(engine, n, ns, integ):
     from diplomjourney_amd.abi import make_problem
     v, b = _case(n, ns, 11)
@@ -89,7 +92,7 @@ def test_gpu_bitwise_equals_replica(engine, n, ns, integ):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("integ", ["rect+rot", "rect", "qk21", "qk21+rot"])
+@pytest.mark.parametrize("integ", ["rect+rot", "rect", "qk21", "qk21+rot", "rect+cum"])
 def test_gpu_irregular_candidates_stream_kernel(engine, integ):
     """Irregular candidates (|beta| > 1.1 at some step; in rotation mode also
     |dphi| > 0.2) leave the streaming kernel's fast loop and are recomputed

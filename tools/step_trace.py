@@ -20,6 +20,24 @@ def main():
         if j - i > best[1] - best[0]:
             best = (i, j)
         i = j + 1 if j > i else i + 1
+    chain = [x for x in seq if x[0] == "k_episode_chain"]
+    if len(chain) > 2 * (best[1] - best[0]):
+        # chained steps: one launch per step; the longest back-to-back run
+        runs, cur = [], [chain[0]]
+        for a, b in zip(chain, chain[1:]):
+            if b[1] - a[2] < 5000:
+                cur.append(b)
+            else:
+                runs.append(cur)
+                cur = [b]
+        runs.append(cur)
+        run = max(runs, key=len)
+        med = lambda v: round(st.median(v) / 1e3, 2)  # noqa: E731
+        print({"label": sys.argv[2] if len(sys.argv) > 2 else "", "steps": len(run),
+               "chain_us": med([e - s for n, s, e in run]),
+               "gap_us": med([run[k + 1][1] - run[k][2] for k in range(len(run) - 1)]),
+               "period_us": med([run[k + 1][1] - run[k][1] for k in range(len(run) - 1)])})
+        return
     run = seq[best[0]:best[1]]
     med = lambda v: round(st.median(v) / 1e3, 2)  # noqa: E731
     out = {"label": sys.argv[2] if len(sys.argv) > 2 else "", "steps": len(run) // 2,
