@@ -212,7 +212,8 @@ def main():
     else:
         ep = DeviceEpisode(eng, n_total, n_steps, rank=rank, world=world,
                            integrator=args.integrator, group=group, log_capacity=8192,
-                           exchange=exchange, chain=not args.no_chain)
+                           exchange=exchange,
+                           chain=not args.no_chain and args.integrator == "rect+cum")
     pool = make_pool(eng, ep, n_steps, args.steps) if inputs == "resident" else None
     main_run = run_steps(args, ep, pool, use_graph, world, device)
     use_graph = main_run["graph"]

@@ -474,6 +474,18 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
       t = __builtin_nan("");
     Kl.h = (t + ecfg.delta_t) - t;                            // consts_from_problem: t_b - t_a
   };
+  // Three steps before the loop ends (blocks whose constants were not final
+  // at the start): wave 0 loads the published words again, in flight with
+  // the last control loads, so the end of the loop normally finds them there.
+  uint64_t w_pre = 0;
+  bool pre_issued = false;
+  auto mid = [&]() {
+    if (waited || pre_issued || s_final) return;
+    pre_issued = true;
+    if (threadIdx.x < kPubWords)
+      w_pre = __hip_atomic_load(&S->chain_pub[threadIdx.x], __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+  };
   // After the loop: the final constants (called by every thread of the block
   // at the same point, see the clamp below).
   auto wait = [&]() {
@@ -486,9 +498,14 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
     __syncthreads();   // LDS reuse
     if (!s_final) {
       if (threadIdx.x < 64) {
+        bool fin = false;
+        if (pre_issued) {
+          const bool ok = threadIdx.x >= kPubWords || static_cast<uint32_t>(w_pre) == epoch;
+          fin = __ballot(!ok) == 0;
+          if (fin && threadIdx.x < kPubWords) s_w[threadIdx.x] = static_cast<uint32_t>(w_pre >> 32);
+        }
         uint32_t it = 0;
-        bool fin;
-        while (!(fin = chain_read(S, epoch, s_w, s_tag)) && ++it < kChainSpinLimit)
+        while (!fin && !(fin = chain_read(S, epoch, s_w, s_tag)) && ++it < kChainSpinLimit)
           __builtin_amdgcn_s_sleep(32);
         if (!fin && threadIdx.x == 0) S->chain_error = 1u;
       }
@@ -506,9 +523,11 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
     const int64_t cl = c0 < n_cand ? c0 : n_cand - CPL;
     double cst[CPL];
     if (pl2)
-      rollout_lane_glds_k<INTEG, ROT, true>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0);
+      rollout_lane_glds_k<INTEG, ROT, true>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0,
+                                            mid);
     else
-      rollout_lane_glds_k<INTEG, ROT, false>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0);
+      rollout_lane_glds_k<INTEG, ROT, false>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0,
+                                             mid);
     Kl = K;            // later tiles: the final constants
     if (c0 < n_cand) {
 #pragma unroll

@@ -287,13 +287,17 @@ struct NoPre {
 // flight; kRotCum only after the loop, which reads Kloop (the step size h and
 // the wheelbase terms; = K except in the chained step, which speculates them
 // in pre0(), called once the first ring slots are in flight).
-template <int INTEG, int ROT, bool PL2, class Pre = NoPre, class Pre0 = NoPre>
+// mid(): kRotCum, called right after the wait of step n_steps - 3: loads it
+// issues complete with that step's last control DMA (the tail waits for both).
+template <int INTEG, int ROT, bool PL2, class Pre = NoPre, class Pre0 = NoPre,
+          class Mid = NoPre>
 __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Consts& Kloop,
                                                     const double* __restrict__ v,
                                                     const double* __restrict__ b, int64_t ld,
                                                     int64_t c0, int n_steps, double (&cst)[2],
                                                     const Pre& pre = Pre{},
-                                                    const Pre0& pre0 = Pre0{}) {
+                                                    const Pre0& pre0 = Pre0{},
+                                                    const Mid& mid = Mid{}) {
   constexpr int CPL = 2;
   constexpr int R = kRing;
   const int lane = threadIdx.x & 63;
@@ -335,6 +339,9 @@ __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Const
           wait_vm<2 * (R - 1)>();   // this step's pair has landed
         } else {
           wait_vm<0>();             // pipeline tail
+        }
+        if constexpr (!std::is_same_v<Mid, NoPre>) {
+          if (st == n_steps - 3) mid();
         }
         v2 = g_ring[wv][u][0][lane];
         b2 = g_ring[wv][u][1][lane];
@@ -461,8 +468,11 @@ __global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(
 #ifndef MPC_STREAM_WAVES
 #define MPC_STREAM_WAVES 5
 #endif
+// kRotCum keeps the start pose's terms live across the loop: at 5 waves it
+// spills (scratch costs far more than the fifth wave gains), so 4.
 template <int INTEG, int ROT, bool KDEV>
-__global__ __launch_bounds__(kBlock, MPC_STREAM_WAVES) void k_rollout_argmin_stream(
+__global__ __launch_bounds__(kBlock, ROT == kRotCum ? 4 : MPC_STREAM_WAVES)
+void k_rollout_argmin_stream(
     Consts Karg, const Consts* __restrict__ Kdev, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part) {
   rollout_argmin_body<kCplWide, INTEG, ROT, false, KDEV>(Karg, Kdev, v, b, n_cand, n_steps,

@@ -13,7 +13,7 @@ fi
 for rep in $(seq ${REPS:-1}); do
 for lib in ${VARS:-intree}; do
 for mode in ${MODES:-rot chain}; do
-  A="--integrator rect+rot"; [ $mode = chain ] && A=""
+  A="--integrator rect+rot"; [ $mode = chain ] && A="--integrator rect+cum"
   L=""; [ $lib != intree ] && L=tools/var_$lib.so
   tag=$lib-$mode$rep
   DIPLOMJOURNEY_MPC_LIB=$L timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/chain/$tag -o run -- python3 bench.py --cpu-seconds 0 --no-second-pass $A > gpurun_out/chain/$tag.json 2> gpurun_out/chain/$tag.err || { tail -5 gpurun_out/chain/$tag.err; exit 1; }

@@ -30,7 +30,7 @@ def main():
     fetch_b = med.get("FETCH_SIZE", 0.0) * 1024.0
     write_b = med.get("WRITE_SIZE", 0.0) * 1024.0
     res = {
-        "kernel": "k_rollout_argmin",
+        "kernel": "k_rollout_argmin_stream",
         "hbm_bytes_per_launch": 2.0 * fetch_b + write_b,
         "algorithmic_bytes_per_launch": algo,
         "fetch_size_bytes_raw": fetch_b, "write_size_bytes": write_b,
