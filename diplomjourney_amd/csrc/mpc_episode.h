@@ -465,8 +465,12 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
     if (s_final) return;
     // speculate h from the published t: the previous step's (+ dt) or, if
     // block 0 already published it, this step's; torn -> NaN (recompute)
-    const uint32_t g0 = s_tag[kConstsWords], g1 = s_tag[kConstsWords + 1];
-    const uint64_t tb = (static_cast<uint64_t>(s_w[kConstsWords + 1]) << 32) | s_w[kConstsWords];
+    const uint32_t g0 = __builtin_amdgcn_readfirstlane(s_tag[kConstsWords]);
+    const uint32_t g1 = __builtin_amdgcn_readfirstlane(s_tag[kConstsWords + 1]);
+    const uint64_t tb =
+        (static_cast<uint64_t>(static_cast<uint32_t>(
+             __builtin_amdgcn_readfirstlane(s_w[kConstsWords + 1]))) << 32) |
+        static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(s_w[kConstsWords]));
     double t = __longlong_as_double(static_cast<long long>(tb));
     if (g0 == g1 && g0 == epoch - 1u)
       t = t + ecfg.delta_t;                                   // episode_prepare

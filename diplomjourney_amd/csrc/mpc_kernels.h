@@ -289,8 +289,10 @@ struct NoPre {
 // in pre0(), called once the first ring slots are in flight).
 // mid(): kRotCum, called right after the wait of step n_steps - 3: loads it
 // issues complete with that step's last control DMA (the tail waits for both).
+// PIN: the leading trig coefficients pinned in VGPRs (8 VGPRs for ~8 VALU per
+// lane-step); off where the register budget is tighter than the VALU budget.
 template <int INTEG, int ROT, bool PL2, class Pre = NoPre, class Pre0 = NoPre,
-          class Mid = NoPre>
+          class Mid = NoPre, bool PIN = true>
 __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Consts& Kloop,
                                                     const double* __restrict__ v,
                                                     const double* __restrict__ b, int64_t ld,
@@ -324,7 +326,8 @@ __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Const
   // leading trig coefficients pinned in VGPRs (opaque to the compiler, so not
   // re-materialised per step)
   trig::Leads lead = trig::const_leads();
-  asm volatile("" : "+v"(lead.tp), "+v"(lead.tq), "+v"(lead.rs), "+v"(lead.rc));
+  if constexpr (PIN)
+    asm volatile("" : "+v"(lead.tp), "+v"(lead.tq), "+v"(lead.rs), "+v"(lead.rc));
 #pragma unroll 1
   for (int s = 0; s < n_steps; s += R) {
 #pragma unroll
@@ -373,8 +376,11 @@ __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Const
     // turns out different — an episode restart reset t — the lane recomputes)
     pre();
     if constexpr (!std::is_same_v<Pre, NoPre>) {
-      if (Kloop.h != K.h) {
-        rollout_lane_glds_k<INTEG, ROT, PL2>(K, K, v, b, ld, c0, n_steps, cst);
+      if (Kloop.h != K.h) {   // rare (episode restart): the per-candidate form,
+        // bitwise the lane's arithmetic (tests/test_replica.py), no second ring loop
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          cst[j] = rollout_candidate_l<INTEG, ROT, PL2>(K, v, b, ld, c0 + j, n_steps, nullptr);
         return;
       }
     }
@@ -395,11 +401,15 @@ __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Const
   }
 }
 
+// kRotCum keeps the start pose's terms live across the loop: with pinned
+// leads it needs > 96 VGPRs and spills at 5 waves/SIMD (any scratch costs far
+// more than the fifth wave gains), unpinned it fits.
 template <int INTEG, int ROT, bool PL2>
 __device__ __forceinline__ void rollout_lane_glds(const Consts& K, const double* __restrict__ v,
                                                   const double* __restrict__ b, int64_t ld,
                                                   int64_t c0, int n_steps, double (&cst)[2]) {
-  rollout_lane_glds_k<INTEG, ROT, PL2>(K, K, v, b, ld, c0, n_steps, cst);
+  rollout_lane_glds_k<INTEG, ROT, PL2, NoPre, NoPre, NoPre, ROT != kRotCum>(
+      K, K, v, b, ld, c0, n_steps, cst);
 }
 
 // L a power of two or not: one loop body each (see step_core).
@@ -468,11 +478,8 @@ __global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(
 #ifndef MPC_STREAM_WAVES
 #define MPC_STREAM_WAVES 5
 #endif
-// kRotCum keeps the start pose's terms live across the loop: at 5 waves it
-// spills (scratch costs far more than the fifth wave gains), so 4.
 template <int INTEG, int ROT, bool KDEV>
-__global__ __launch_bounds__(kBlock, ROT == kRotCum ? 4 : MPC_STREAM_WAVES)
-void k_rollout_argmin_stream(
+__global__ __launch_bounds__(kBlock, MPC_STREAM_WAVES) void k_rollout_argmin_stream(
     Consts Karg, const Consts* __restrict__ Kdev, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part) {
   rollout_argmin_body<kCplWide, INTEG, ROT, false, KDEV>(Karg, Kdev, v, b, n_cand, n_steps,
