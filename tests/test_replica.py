@@ -100,7 +100,8 @@ def test_gpu_irregular_candidates_stream_kernel(engine, integ):
     cost and trajectory equal the host replica bit for bit: (a) most
     candidates irregular, irregular winner; (b) a few irregular candidates
     scattered over otherwise regular blocks; (c) 2.1e6 candidates, so blocks
-    stride over several tiles, with irregular candidates only in late tiles."""
+    stride over several tiles, with irregular candidates only in late tiles;
+    (d) huge arguments (Payne-Hanek reduction on the device)."""
     from diplomjourney_amd.abi import make_problem
     rng = np.random.default_rng(3)
     p = make_problem(0, 0, 0, 0.3, 0.8, 0, 0, 0.5, 0.05, 0.1)
@@ -114,6 +115,15 @@ def test_gpu_irregular_candidates_stream_kernel(engine, integ):
     n = 2 * 2048 * 512 + 1000
     v, b = _case(n, 4, 13)
     b[2, [2048 * 512 + 7, n - 3, n - 600]] = -1.15
+    cases.append((v, b, None))
+    # (d) huge steering angles and headings: the safe recurrence's trig takes
+    # the Payne-Hanek reduction (mpc_trig.h reduce_pio2_large) on the device,
+    # bit for bit the host's
+    n, ns = 50_000, 6
+    v, b = _case(n, ns, 14)
+    hit = rng.choice(n, 64, replace=False)
+    b[1, hit[:32]] = rng.uniform(1e6, 1e300, 32) * rng.choice([-1, 1], 32)
+    v[3, hit[32:]] = rng.uniform(1e7, 1e12, 32)        # dphi and the heading become huge
     cases.append((v, b, None))
     for v, b, want_irregular in cases:
         st, costs = replica_rollout(p, v, b, integ)
