@@ -323,16 +323,24 @@ def run_steps(args, ep, pool, use_graph, world, device):
         step(i)
     flush()
     Ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
-    kern = [(Ev(), Ev()) for _ in range(args.steps)]
+    # latency pass: one event per step start (more events per step would add
+    # their own host cost to an eagerly launched step)
     marks = [Ev() for _ in range(args.steps + 1)]
     torch.cuda.synchronize()
     for i in range(args.steps):
         marks[i].record()
-        step(i, kern[i])
+        step(i)
     marks[-1].record()
     flush()
     torch.cuda.synchronize()
     step_gpu_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)]
+    # the rollout launch inside eager steps, events around it
+    n_kern = min(args.steps, 100)
+    kern = [(Ev(), Ev()) for _ in range(n_kern)]
+    for i in range(n_kern):
+        step(i, kern[i])
+    flush()
+    torch.cuda.synchronize()
     # Throughput pass: the K steps captured once into a HIP graph (the episode
     # lives in HBM, so a replay simply continues it) and replayed: no host
     # cost between the step's kernels.  Multi-GPU runs capture the RCCL

@@ -417,6 +417,17 @@ int mpc_episode_finalize(void* state, const double* v_sc, const double* beta_sc,
   return last_hip_status();
 }
 
+int mpc_episode_step(void* state, const double* v_sc, const double* beta_sc, int64_t n_cand,
+                     int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
+                     size_t ws_bytes, mpc_result_t* out, const mpc_episode_config_t* advance,
+                     mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream) {
+  const int a =
+      mpc_episode_partials(state, v_sc, beta_sc, n_cand, n_steps, integrator, ws, ws_bytes, stream);
+  if (a != MPC_OK) return a;
+  return mpc_episode_finalize(state, v_sc, beta_sc, n_cand, n_steps, index_base, integrator, ws,
+                              ws_bytes, out, advance, log, log_capacity, stream);
+}
+
 int mpc_episode_rollout(void* state, const double* v_sc, const double* beta_sc, int64_t n_cand,
                         int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
                         size_t ws_bytes, mpc_result_t* out, const mpc_episode_config_t* advance,

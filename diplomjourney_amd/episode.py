@@ -216,6 +216,7 @@ class DeviceEpisode:
         self._ws = [self.ws, torch.empty_like(self.ws)] if self.chain else [self.ws]
         self._pending = None
         self._epoch = 0
+        self._checked = {}
         self.steps_enqueued = 0
         self.reset()
 
@@ -230,12 +231,17 @@ class DeviceEpisode:
 
     def _check_controls(self, controls):
         v, b = controls
+        key = (id(v), id(b), v.data_ptr(), b.data_ptr())
+        if key in self._checked:         # a resident batch seen before: checked once
+            return v, b
         if (tuple(v.shape) != (self.n_steps, self.n_local) or v.shape != b.shape
                 or v.dtype != torch.float64 or b.dtype != torch.float64
                 or not v.is_contiguous() or not b.is_contiguous()
                 or v.device != self.v_sc.device or b.device != self.v_sc.device):
             raise ValueError("controls must be contiguous float64 [n_steps, n_local] "
                              "tensors on the episode's device")
+        if len(self._checked) < 4096:
+            self._checked[key] = (v, b)   # holds the tensors: ids stay unique
         return v, b
 
     def _chain_step(self, controls, events=None):
@@ -333,9 +339,12 @@ class DeviceEpisode:
                 self.log.data_ptr() if one_gpu else None, self.log_capacity if one_gpu else 0, st)
         if events:
             events[0].record()
-        if self.split:
-            # streaming kernel, then the selection kernel (two launches; the
-            # faster form on MI355X: 44.8 vs 47.5 us per config-C step)
+        if self.split and not events:
+            # streaming kernel, then the selection kernel: two launches in one
+            # host call (the faster form on MI355X: 44.8 vs 47.5 us per
+            # config-C step than the one-launch form below)
+            native.check(L.mpc_episode_step(*args), "mpc_episode_step")
+        elif self.split:
             self.partials(st)
             native.check(L.mpc_episode_finalize(*args), "mpc_episode_finalize")
         else:

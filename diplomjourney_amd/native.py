@@ -30,7 +30,7 @@ EXPORTS = (
     "mpc_batched_workspace_bytes", "mpc_rollout_argmin_batched", "mpc_select_winner",
     "mpc_sample_controls", "mpc_episode_state_bytes", "mpc_episode_reset",
     "mpc_episode_expand", "mpc_episode_advance", "mpc_episode_sample", "mpc_episode_partials",
-    "mpc_episode_finalize", "mpc_episode_rollout", "mpc_episode_chain_step",
+    "mpc_episode_finalize", "mpc_episode_rollout", "mpc_episode_step", "mpc_episode_chain_step",
     "mpc_episode_chain_error",
     "mpc_fulltree_workspace_bytes", "mpc_fulltree_argmin",
     "mpc_fulltree_batched_workspace_bytes", "mpc_fulltree_argmin_batched",
@@ -136,6 +136,8 @@ def lib():
     L.mpc_fulltree_argmin_batched.argtypes = [_P, _P, _I32, ctypes.c_double, ctypes.c_double,
                                               ctypes.c_double, _P, _I32, _P, _I32, _I32, _P,
                                               ctypes.c_size_t, _P, _P]
+    L.mpc_episode_step.restype = ctypes.c_int
+    L.mpc_episode_step.argtypes = L.mpc_episode_finalize.argtypes
     L.mpc_episode_chain_step.restype = ctypes.c_int
     L.mpc_episode_chain_step.argtypes = [ctypes.POINTER(MpcEpisodeConfig), _P, _I32,
                                          ctypes.c_uint32, _P, _P,

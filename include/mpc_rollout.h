@@ -224,6 +224,12 @@ int mpc_episode_finalize(void* state, const double* v_sc, const double* beta_sc,
                          int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
                          size_t ws_bytes, mpc_result_t* out, const mpc_episode_config_t* advance,
                          mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
+/* mpc_episode_partials + mpc_episode_finalize in one call (the two launches
+ * of a step; one host call per step on an eagerly launched episode). */
+int mpc_episode_step(void* state, const double* v_sc, const double* beta_sc, int64_t n_cand,
+                     int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
+                     size_t ws_bytes, mpc_result_t* out, const mpc_episode_config_t* advance,
+                     mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
 
 /* Chained step (integrator MPC_INTEG_RECT | MPC_HEADING_CUMULATIVE): ONE
  * launch = the streaming rollout of this step (v_sc / beta_sc, records into
