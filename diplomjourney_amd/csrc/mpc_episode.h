@@ -425,9 +425,6 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
     int n_gathered, mpc_episode_config_t ecfg, mpc_episode_log_t* __restrict__ log, int cap) {
   static_assert(ROT == kRotCum, "chained steps need the pose-independent recurrence");
   if (blockIdx.x == 0) {
-#ifdef MPC_CHAIN_NOFIN
-    has_prev = 0;   // A/B probe only
-#endif
     if (has_prev) {
       if constexpr (MODE == kChainFin) {
         const Consts Kp = S->h.K;
@@ -495,10 +492,6 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
   auto wait = [&]() {
     if (waited) return;
     waited = true;
-#ifdef MPC_CHAIN_NOWAIT
-    K = Kl;   // A/B probe only
-    return;
-#endif
     __syncthreads();   // LDS reuse
     if (!s_final) {
       if (threadIdx.x < 64) {
