@@ -98,6 +98,9 @@ def parse():
                          "input); sampled: the device sampler regenerates them per step")
     ap.add_argument("--no-second-pass", action="store_true",
                     help="skip the comparison run with the other --inputs mode")
+    ap.add_argument("--fused", action="store_true",
+                    help="one launch per step: the rollout's last block runs the selection "
+                         "(mpc_episode_rollout) instead of a separate selection launch")
     ap.add_argument("--no-chain", action="store_true",
                     help="separate selection launch per step instead of chained steps "
                          "(mpc_episode_chain_step: the step's launch completes the previous step)")
@@ -212,7 +215,7 @@ def main():
     else:
         ep = DeviceEpisode(eng, n_total, n_steps, rank=rank, world=world,
                            integrator=args.integrator, group=group, log_capacity=8192,
-                           exchange=exchange,
+                           exchange=exchange, split=not args.fused,
                            chain=not args.no_chain and args.integrator == "rect+cum")
     pool = make_pool(eng, ep, n_steps, args.steps) if inputs == "resident" else None
     main_run = run_steps(args, ep, pool, use_graph, world, device)
