@@ -213,20 +213,18 @@ __device__ __forceinline__ double tr_at(const Winner& r, int k, int q) {
 // Episode._advance: finishing logic (:392-414), events (:564-569), restart.
 // Operates on a register copy of the episode scalars (the caller loads it
 // once and stores it back once).
+// The step's log record is filled in `L` (LDS); the caller stores it
+// (log_slot) together with the head.
 __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeHead& H,
-                                       const Winner& r, mpc_episode_log_t* __restrict__ log,
-                                       int cap) {
+                                       const Winner& r, mpc_episode_log_t& L) {
   EpisodeHead* S = &H;
   S->steps_for_slowing -= 1;
   S->incumbent = 9223372036854775808.0;  // float(sys.maxsize), :428
-  mpc_episode_log_t* L = (log && cap > 0) ? &log[S->step % cap] : nullptr;
-  if (L) {
-    L->step = S->step;
-    L->index = r.found ? r.index : -1;
-    L->p = S->p;
-    L->episode = S->episodes;
-    L->cost = r.cost;
-  }
+  L.step = S->step;
+  L.index = r.found ? r.index : -1;
+  L.p = S->p;
+  L.episode = S->episodes;
+  L.cost = r.cost;
   S->step += 1;
   if (r.found) {
     const int last = r.n_steps - 1;
@@ -275,49 +273,68 @@ __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeHea
     const double ex = S->x_t - S->x, ey = S->y_t - S->y;
     if (ex * ex + ey * ey <= c.eps || S->p > c.max_steps) episode_restart(c, *S);
   }
+#ifdef MPC_FIN_TRACE
+  g_fin_tick[1] = __builtin_amdgcn_s_memrealtime();
+#endif
   episode_prepare(c, *S);
-  if (L) {
-    L->x = S->x;
-    L->y = S->y;
-    L->phi = S->phi;
-    L->v = S->v;
-    L->beta = S->beta;
-  }
+#ifdef MPC_FIN_TRACE
+  g_fin_tick[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+  L.x = S->x;
+  L.y = S->y;
+  L.phi = S->phi;
+  L.v = S->v;
+  L.beta = S->beta;
 }
 
 __device__ void episode_hook(const mpc_episode_config_t& c, const EpisodeHook& h,
-                             const Winner& r, EpisodeHead& H) {
-  episode_advance(c, H, r, h.log, h.cap);
+                             const Winner& r, EpisodeHead& H, mpc_episode_log_t& L,
+                             mpc_episode_log_t*& slot) {
+  slot = log_slot(h.log, h.cap, H.step);
+  episode_advance(c, H, r, L);
 }
 
 // Multi-GPU: lexicographic (cost, global index) selection over the gathered
 // per-rank winners (the all-reduce(min+index)), then the episode update.
+// Called by every thread of a block (>= 64 threads): thread 0 updates a
+// register copy of the head, which goes back to HBM through LDS one word per
+// lane (a single lane's stores serialise); end_chain clears the chain tags.
 __device__ inline void advance_from_results(const mpc_episode_config_t& c, EpisodeState* S,
                                             const mpc_result_t* __restrict__ res, int n,
-                                            mpc_episode_log_t* __restrict__ log, int cap) {
-  EpisodeHead H = S->h;
-  uint64_t bk;
-  const int best = select_index(res, n, bk);
-  const mpc_result_t& r = res[best];
-  Winner w;
-  w.cost = r.cost;
-  w.index = r.index;
-  w.found = (bk != ~0ull && r.cost < H.incumbent) ? 1 : 0;
-  w.n_steps = r.n_steps;
-  w.v = r.v;
-  w.beta = r.beta;
-  for (int k = 0; k < 3; ++k)
-    for (int q = 0; q < 3; ++q) w.tr[k][q] = r.traj[k < r.n_steps ? k : 0][q];
-  episode_advance(c, H, w, log, cap);
-  S->h = H;
+                                            mpc_episode_log_t* __restrict__ log, int cap,
+                                            bool end_chain = true) {
+  __shared__ uint64_t s_head[kHeadWords];
+  __shared__ mpc_episode_log_t s_log;
+  __shared__ mpc_episode_log_t* s_slot;
+  if (threadIdx.x == 0) {
+    EpisodeHead H = S->h;
+    uint64_t bk;
+    const int best = select_index(res, n, bk);
+    const mpc_result_t& r = res[best];
+    Winner w;
+    w.cost = r.cost;
+    w.index = r.index;
+    w.found = (bk != ~0ull && r.cost < H.incumbent) ? 1 : 0;
+    w.n_steps = r.n_steps;
+    w.v = r.v;
+    w.beta = r.beta;
+    for (int k = 0; k < 3; ++k)
+      for (int q = 0; q < 3; ++q) w.tr[k][q] = r.traj[k < r.n_steps ? k : 0][q];
+    s_slot = log_slot(log, cap, H.step);
+    episode_advance(c, H, w, s_log);
+    __builtin_memcpy(s_head, &H, sizeof(EpisodeHead));
+  }
+  __syncthreads();
+  store_update(&S->h, s_head, s_slot, reinterpret_cast<const uint64_t*>(&s_log),
+               end_chain ? S->chain_pub : nullptr, kPubWords);
 }
 
-__global__ void k_episode_advance(mpc_episode_config_t c, EpisodeState* __restrict__ S,
-                                  const mpc_result_t* __restrict__ res, int n,
-                                  mpc_episode_log_t* __restrict__ log, int cap) {
-  if (threadIdx.x != 0) return;
+__global__ __launch_bounds__(64) void k_episode_advance(mpc_episode_config_t c,
+                                                        EpisodeState* __restrict__ S,
+                                                        const mpc_result_t* __restrict__ res,
+                                                        int n, mpc_episode_log_t* __restrict__ log,
+                                                        int cap) {
   advance_from_results(c, S, res, n, log, cap);
-  for (int q = 0; q < kPubWords; ++q) S->chain_pub[q] = 0ull;   // ends a chain of chained steps
 }
 
 // ---------------------------------------------------------------------------
@@ -433,7 +450,7 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
                                                         b_prev, n_cand, n_steps, index_base,
                                                         S->h.incumbent, out_prev, ecfg, hook);
       } else {
-        if (threadIdx.x == 0) advance_from_results(ecfg, S, gathered, n_gathered, log, cap);
+        advance_from_results(ecfg, S, gathered, n_gathered, log, cap, false);
       }
     }
     chain_publish(S, epoch);

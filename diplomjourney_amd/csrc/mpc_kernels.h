@@ -577,63 +577,70 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
       trig::sincos_fast(s_phi[lane], &s_a[lane], &s_c[lane]);  // == sincos_core if regular
     __syncthreads();
   }
-  if (lane != 0) return;
-  out->n_steps = n_steps;
-  if (win) win->n_steps = n_steps;
-  if (!valid) {
-    out->cost = __builtin_inf();
-    out->index = -1;
-    out->found = 0;
-    out->v = 0.0;
-    out->beta = 0.0;
-    if (win) {
-      win->cost = __builtin_inf();
-      win->index = -1;
-      win->found = 0;
-    }
-    return;
-  }
-  const double c = key_cost(key);
-  const int found = c < incumbent ? 1 : 0;
-  out->cost = c;
-  out->index = s_rep;
-  out->found = found;
-  out->v = s_v[0];
-  out->beta = s_b0;
-  if (win) {
-    win->cost = c;
-    win->index = s_rep;
-    win->found = found;
-    win->v = s_v[0];
-    win->beta = s_b0;
-  }
-  double x, y, sn, cs, ph;
-  if (fast)
-    step_start<ROT>(K, x, y, ph, sn, cs);    // kRotCum: identity rotation, empty sums
-  else
-    step_start<0>(K, x, y, ph, sn, cs);
-  for (int st = 0; st < n_steps; ++st) {
-    if (fast) {
-      ph = ph + s_dphi[st];
-      trig::rotate_by(s_a[st], s_c[st], sn, cs);
+  // Lane 0 runs the serial pass into LDS; the record's trajectory is then
+  // stored by one lane per value (a single lane's ~30 stores would serialise
+  // in the address path for ~1 us).
+  __shared__ double s_tr[MPC_MAX_STEPS * 3];
+  if (lane == 0) {
+    out->n_steps = n_steps;
+    if (win) win->n_steps = n_steps;
+    if (!valid) {
+      out->cost = __builtin_inf();
+      out->index = -1;
+      out->found = 0;
+      out->v = 0.0;
+      out->beta = 0.0;
+      if (win) {
+        win->cost = __builtin_inf();
+        win->index = -1;
+        win->found = 0;
+      }
     } else {
-      ph = s_phi[st];
-      sn = s_a[st];
-      cs = s_c[st];
-    }
-    x = position_step<INTEG>(x, s_v[st], cs, K);
-    y = position_step<INTEG>(y, s_v[st], sn, K);
-    double px = x, py = y;
-    if (ROT == kRotCum && fast) cum_pose(K, x, y, px, py);
-    out->traj[st][0] = px;
-    out->traj[st][1] = py;
-    out->traj[st][2] = ph;
-    if (win && st < 3) {
-      win->tr[st][0] = px;
-      win->tr[st][1] = py;
-      win->tr[st][2] = ph;
+      const double c = key_cost(key);
+      const int found = c < incumbent ? 1 : 0;
+      out->cost = c;
+      out->index = s_rep;
+      out->found = found;
+      out->v = s_v[0];
+      out->beta = s_b0;
+      if (win) {
+        win->cost = c;
+        win->index = s_rep;
+        win->found = found;
+        win->v = s_v[0];
+        win->beta = s_b0;
+      }
+      double x, y, sn, cs, ph;
+      if (fast)
+        step_start<ROT>(K, x, y, ph, sn, cs);    // kRotCum: identity rotation, empty sums
+      else
+        step_start<0>(K, x, y, ph, sn, cs);
+      for (int st = 0; st < n_steps; ++st) {
+        if (fast) {
+          ph = ph + s_dphi[st];
+          trig::rotate_by(s_a[st], s_c[st], sn, cs);
+        } else {
+          ph = s_phi[st];
+          sn = s_a[st];
+          cs = s_c[st];
+        }
+        x = position_step<INTEG>(x, s_v[st], cs, K);
+        y = position_step<INTEG>(y, s_v[st], sn, K);
+        double px = x, py = y;
+        if (ROT == kRotCum && fast) cum_pose(K, x, y, px, py);
+        s_tr[3 * st] = px;
+        s_tr[3 * st + 1] = py;
+        s_tr[3 * st + 2] = ph;
+        if (win && st < 3) {
+          win->tr[st][0] = px;
+          win->tr[st][1] = py;
+          win->tr[st][2] = ph;
+        }
+      }
     }
   }
+  __syncthreads();
+  if (valid && lane < 3 * n_steps) (&out->traj[0][0])[lane] = s_tr[lane];
 }
 
 // The device-resident episode's scalars (mpc_episode.h: EpisodeState = this
@@ -657,8 +664,31 @@ struct EpisodeHook {  // single-GPU episode: finalize also advances it
   uint64_t* chain_pub = nullptr;   // cleared with the update (ends a chain of chained steps)
   int chain_pub_words = 0;
 };
+constexpr int kHeadWords = static_cast<int>(sizeof(EpisodeHead) / 8);
+constexpr int kLogWords = static_cast<int>(sizeof(mpc_episode_log_t) / 8);
+static_assert(sizeof(EpisodeHead) % 8 == 0 && kHeadWords <= 64, "head: one word per lane");
+static_assert(sizeof(mpc_episode_log_t) % 8 == 0 && kLogWords <= 64, "log: one word per lane");
+
+__device__ __forceinline__ mpc_episode_log_t* log_slot(mpc_episode_log_t* log, int cap,
+                                                       int64_t step) {
+  return (log && cap > 0) ? &log[step % cap] : nullptr;
+}
+
+// The episode update's stores, one 8-B word per lane (called by every thread
+// after a barrier; thread 0 staged the head and the log record in LDS): a
+// single lane's ~40 stores serialise in the address path for ~0.7 us.
+__device__ __forceinline__ void store_update(EpisodeHead* H, const uint64_t* s_head,
+                                             mpc_episode_log_t* slot, const uint64_t* s_log,
+                                             uint64_t* chain_pub, int chain_words) {
+  const int q = threadIdx.x;
+  if (q < kHeadWords) reinterpret_cast<uint64_t*>(H)[q] = s_head[q];
+  if (slot && q < kLogWords) reinterpret_cast<uint64_t*>(slot)[q] = s_log[q];
+  if (chain_pub && q < chain_words) chain_pub[q] = 0ull;
+}
+
 __device__ void episode_hook(const mpc_episode_config_t& c, const EpisodeHook& h,
-                             const Winner& r, EpisodeHead& H);
+                             const Winner& r, EpisodeHead& H, mpc_episode_log_t& L,
+                             mpc_episode_log_t*& slot);
 
 // Block-record reduction + winner re-roll (+ episode update), run by every
 // thread of one block of NT threads.  SC1: the records were written by
@@ -686,6 +716,9 @@ __device__ __forceinline__ void load8_rec_sc1(const Rec* const (&p)[8], u64x2 (&
       : "memory");
 }
 
+#ifdef MPC_FIN_TRACE
+__device__ uint64_t g_fin_tick[4];   // debug builds only: stage ticks inside the hook
+#endif
 template <int INTEG, int ROT, bool KDEV, int NT, bool SC1>
 __device__ __forceinline__ void finalize_block(
     const Rec* __restrict__ part, int n_part, const Consts& K, const double* __restrict__ v,
@@ -699,9 +732,11 @@ __device__ __forceinline__ void finalize_block(
   // 8-B vector load per lane, issued after its record loads) and updated by
   // thread 0 once the winner is known.  (Loading them into thread 0's SGPRs
   // serialised three scalar round trips in front of wave 0's record loads.)
-  constexpr int kHeadWords = static_cast<int>(sizeof(EpisodeHead) / 8);
-  static_assert(sizeof(EpisodeHead) % 8 == 0 && kHeadWords <= 64 && NT >= 128, "head staging");
+  static_assert(NT >= 128, "head staging by wave 1");
+  static_assert(MPC_MAX_STEPS * 3 <= NT, "trajectory stored one value per lane");
   __shared__ uint64_t s_head[kHeadWords];
+  __shared__ mpc_episode_log_t s_log;   // filled field by field by the update
+  __shared__ mpc_episode_log_t* s_slot;
   __shared__ uint64_t s_key[NT / 64];
   __shared__ int64_t s_idx[NT / 64];
   uint64_t k = ~0ull;
@@ -765,12 +800,20 @@ __device__ __forceinline__ void finalize_block(
 #ifdef MPC_FIN_TRACE
   const uint64_t tr2 = __builtin_amdgcn_s_memrealtime();
 #endif
-  if (KDEV && hook.H && threadIdx.x == 0) {   // emit_winner ended with a barrier
-    EpisodeHead H;
-    __builtin_memcpy(&H, s_head, sizeof(EpisodeHead));
-    episode_hook(ecfg, hook, w, H);
-    *hook.H = H;
-    for (int q = 0; q < hook.chain_pub_words; ++q) hook.chain_pub[q] = 0ull;
+  if (KDEV && hook.H) {
+    if (threadIdx.x == 0) {   // emit_winner ended with a barrier
+      EpisodeHead H;
+      __builtin_memcpy(&H, s_head, sizeof(EpisodeHead));
+#ifdef MPC_FIN_TRACE
+      g_fin_tick[0] = __builtin_amdgcn_s_memrealtime();
+#endif
+      episode_hook(ecfg, hook, w, H, s_log, s_slot);
+      __builtin_memcpy(s_head, &H, sizeof(EpisodeHead));
+    }
+    __syncthreads();
+    // the head and the log record back to HBM, the chain tags cleared
+    store_update(hook.H, s_head, s_slot, reinterpret_cast<const uint64_t*>(&s_log),
+                 hook.chain_pub, hook.chain_pub_words);
   }
 #ifdef MPC_FIN_TRACE
   if (threadIdx.x == 0) {   // debug builds only: 10-ns ticks in unused trajectory slots
@@ -778,6 +821,9 @@ __device__ __forceinline__ void finalize_block(
     out->traj[31][0] = static_cast<double>(tr1 - tr0);
     out->traj[31][1] = static_cast<double>(tr2 - tr1);
     out->traj[31][2] = static_cast<double>(tr3 - tr2);
+    out->traj[30][0] = static_cast<double>(g_fin_tick[0] - tr2);
+    out->traj[30][1] = static_cast<double>(g_fin_tick[1] - g_fin_tick[0]);
+    out->traj[30][2] = static_cast<double>(g_fin_tick[2] - g_fin_tick[1]);
   }
 #endif
 }

@@ -24,6 +24,7 @@ for i in range(30):
     ep.step(controls=pool[i % 4])
     torch.cuda.synchronize()
     r = result_from_bytes(ep.local.cpu().numpy().tobytes())
-    rows.append([r.traj[31][0], r.traj[31][1], r.traj[31][2]])
+    rows.append([r.traj[31][0], r.traj[31][1], r.traj[31][2], r.traj[30][0], r.traj[30][1], r.traj[30][2]])
 a = np.array(rows[5:]) * 0.01
-print("finalize stages (us): reduce+H %.2f  emit %.2f  hook %.2f" % tuple(np.median(a, axis=0)))
+print("finalize stages (us): reduce+H %.2f  emit %.2f  hook %.2f "
+      "(copy-in %.2f, advance %.2f, prepare %.2f)" % tuple(np.median(a, axis=0)))
