@@ -432,10 +432,13 @@ __device__ __forceinline__ bool chain_read(const EpisodeState* S, uint32_t epoch
 #ifndef MPC_CHAIN_WAVES
 #define MPC_CHAIN_WAVES 4   // launch bound of the chained kernel (5 spills: block 0's finalize)
 #endif
-template <int INTEG, int ROT, int MODE>
+// PL2 (wheelbase a power of two) is a template parameter, not a runtime
+// branch: with both rollout variants inlined the kernel held 119 VGPRs and
+// spilled 191 SGPRs; one variant per instantiation: 108-112 VGPRs, 81-86.
+template <int INTEG, int ROT, int MODE, bool PL2>
 __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
     EpisodeState* __restrict__ S, uint32_t epoch, const double* __restrict__ v,
-    const double* __restrict__ b, int64_t n_cand, int n_steps, int pl2, Rec* __restrict__ part,
+    const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part,
     int has_prev, const Rec* __restrict__ part_prev, int n_part_prev,
     const double* __restrict__ v_prev, const double* __restrict__ b_prev, int64_t index_base,
     mpc_result_t* __restrict__ out_prev, const mpc_result_t* __restrict__ gathered,
@@ -536,12 +539,7 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
     // ignored), so every lane reaches the barriers of pre0 / wait on the same path
     const int64_t cl = c0 < n_cand ? c0 : n_cand - CPL;
     double cst[CPL];
-    if (pl2)
-      rollout_lane_glds_k<INTEG, ROT, true>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0,
-                                            mid);
-    else
-      rollout_lane_glds_k<INTEG, ROT, false>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0,
-                                             mid);
+    rollout_lane_glds_k<INTEG, ROT, PL2>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0, mid);
     Kl = K;            // later tiles: the final constants
     if (c0 < n_cand) {
 #pragma unroll

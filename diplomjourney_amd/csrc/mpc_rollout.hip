@@ -491,15 +491,22 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
   const int n_part_prev = static_cast<int>(rollout_grid<kCplWide>(n_cand));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   constexpr int I = MPC_INTEG_RECT;
-  if (mode == MPC_CHAIN_FINALIZE)
-    k_episode_chain<I, kRotCum, kChainFin><<<grid, kBlock, 0, st>>>(
-        S, epoch, v_sc, beta_sc, n_cand, n_steps, pl2, static_cast<Rec*>(ws), has_prev,
-        static_cast<const Rec*>(ws_prev), n_part_prev, v_prev, beta_prev, index_base, out_prev,
-        nullptr, 0, *cfg, log, log_capacity);
+  auto launch = [&](auto pl2_tag) {
+    constexpr bool P = decltype(pl2_tag)::value;
+    if (mode == MPC_CHAIN_FINALIZE)
+      k_episode_chain<I, kRotCum, kChainFin, P><<<grid, kBlock, 0, st>>>(
+          S, epoch, v_sc, beta_sc, n_cand, n_steps, static_cast<Rec*>(ws), has_prev,
+          static_cast<const Rec*>(ws_prev), n_part_prev, v_prev, beta_prev, index_base, out_prev,
+          nullptr, 0, *cfg, log, log_capacity);
+    else
+      k_episode_chain<I, kRotCum, kChainAdv, P><<<grid, kBlock, 0, st>>>(
+          S, epoch, v_sc, beta_sc, n_cand, n_steps, static_cast<Rec*>(ws), has_prev, nullptr, 0,
+          nullptr, nullptr, index_base, nullptr, gathered, n_gathered, *cfg, log, log_capacity);
+  };
+  if (pl2)
+    launch(std::true_type{});
   else
-    k_episode_chain<I, kRotCum, kChainAdv><<<grid, kBlock, 0, st>>>(
-        S, epoch, v_sc, beta_sc, n_cand, n_steps, pl2, static_cast<Rec*>(ws), has_prev, nullptr,
-        0, nullptr, nullptr, index_base, nullptr, gathered, n_gathered, *cfg, log, log_capacity);
+    launch(std::false_type{});
   return last_hip_status();
 }
 
