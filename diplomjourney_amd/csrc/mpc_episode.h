@@ -457,6 +457,12 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
       }
     }
     chain_publish(S, epoch);
+    // The host picked PL2 from the caller's cfg; the tile blocks use the
+    // published head's wheelbase terms.  If those disagree (a cfg other than
+    // the one the state was reset with) every dphi would be formed with the
+    // wrong form: flag it (chain_error = 2) instead of returning wrong costs
+    // silently.  (chain_publish ended with a barrier after the head store.)
+    if (threadIdx.x == 0 && (S->h.K.L_pow2 != 0) != PL2) S->chain_error = 2u;
     return;
   }
   constexpr int CPL = 2;

@@ -178,7 +178,7 @@ class DeviceEpisode:
 
     def __init__(self, engine, n_cand_total, n_steps, rank=0, world=1, seed=20261015,
                  integrator="rect", group=None, start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3),
-                 log_capacity=4096, split=True, exchange=None, chain=False):
+                 log_capacity=4096, split=True, exchange=None, chain=False, L=None):
         self.eng = engine
         self.lib = native.lib()
         self.n_total = int(n_cand_total)
@@ -188,6 +188,8 @@ class DeviceEpisode:
         self.n_local = self.hi - self.lo
         self.integrator = integrator
         self.cfg = reference_episode_config(start, target, seed)
+        if L is not None:                 # wheelbase other than config.py's (tests: L not 2^k)
+            self.cfg.L = float(L)
         dev = engine.device
         self.state = torch.zeros(self.lib.mpc_episode_state_bytes(), dtype=torch.uint8,
                                  device=dev)

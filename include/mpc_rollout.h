@@ -247,7 +247,10 @@ int mpc_episode_step(void* state, const double* v_sc, const double* beta_sc, int
  * mpc_episode_advance (multi-GPU); either ends the chain.  epoch: nonzero,
  * different from the previous chained launch's.  Aligned path only (n_cand
  * even, 16-B aligned controls): MPC_ERR_UNSUPPORTED otherwise.  ws / ws_prev:
- * two workspaces of mpc_workspace_bytes(n_cand, n_steps) each, alternated. */
+ * two workspaces of mpc_workspace_bytes(n_cand, n_steps) each, alternated.
+ * cfg must be the configuration the state was reset with: the launch picks
+ * its wheelbase form (L a power of two or not) from cfg->L, the rollout uses
+ * the state's constants; a mismatch sets chain error 2 (mpc_episode_chain_error). */
 #define MPC_CHAIN_FINALIZE 1
 #define MPC_CHAIN_ADVANCE 2
 int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t mode,
@@ -258,8 +261,9 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
                            const double* beta_prev, mpc_result_t* out_prev,
                            const mpc_result_t* gathered, int32_t n_gathered,
                            mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
-/* Nonzero if a chained step's wait for its constants ever timed out (the
- * launch then ran on stale constants); reads the device state (syncs). */
+/* Nonzero if a chained step went wrong: 1 = its wait for the published
+ * constants timed out (the launch then ran on stale constants); 2 = cfg's
+ * wheelbase form disagreed with the state's.  Reads the device state (syncs). */
 int mpc_episode_chain_error(const void* state, int32_t* error, mpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------

@@ -399,27 +399,30 @@ def _episode_log(ep):
             for r in ep.read_log()]
 
 
-@pytest.mark.parametrize("integ", ["rect+cum"])
-def test_chained_episode_matches_separate_launches(engine, integ):
+@pytest.mark.parametrize("wheelbase", [0.5, 0.45])
+def test_chained_episode_matches_separate_launches(engine, wheelbase):
     """Chained steps (mpc_episode_chain_step: step k's rollout and step k-1's
     finalize + episode update in ONE launch, the tile blocks waiting on device
     for block 0's published constants) log exactly the steps of the
     two-launch device episode over 130 steps of resident batches — operator
     events at p = 60/90/110 included — eagerly and replayed from a HIP graph
     whose last launch is the flush; a launch whose last tile is partial
-    (50_000 = 97 tiles of 512 + 336)."""
+    (50_000 = 97 tiles of 512 + 336).  Both wheelbase forms of the chained
+    kernel: L = 0.5 (a power of two, PL2) and L = 0.45 (v / L divided)."""
     from diplomjourney_amd import math_model_tree as mmt
     from diplomjourney_amd.episode import DeviceEpisode
+    integ = "rect+cum"
     n, ns, steps = 50_000, 10, 130
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
     pool = [engine.sample_controls(V, B, n, ns, 500 + i) for i in range(8)]
-    ref = DeviceEpisode(engine, n, ns, integrator=integ, log_capacity=256)
+    ref = DeviceEpisode(engine, n, ns, integrator=integ, log_capacity=256, L=wheelbase)
     for i in range(steps):
         ref.step(controls=pool[i % 8])
     want = _episode_log(ref)
     assert len(want) == steps and {r[8] for r in want} >= {60, 90, 110}
-    ch = DeviceEpisode(engine, n, ns, integrator=integ, log_capacity=256, chain=True)
+    ch = DeviceEpisode(engine, n, ns, integrator=integ, log_capacity=256, chain=True,
+                       L=wheelbase)
     half = steps // 2
     for i in range(half):
         ch.step(controls=pool[i % 8])
@@ -456,11 +459,32 @@ def test_chained_episode_multi_tile_blocks(engine):
     assert ch.chain_error() == 0
 
 
-def test_chained_exchange_path_and_graph_capture(engine):
+def test_chained_wheelbase_mismatch_is_flagged(engine):
+    """A chained launch whose cfg wheelbase form (power of two or not)
+    differs from the state's constants sets chain error 2 instead of
+    returning wrong costs silently."""
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.episode import DeviceEpisode
+    n, ns = 20_000, 10
+    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
+    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
+    pool = [engine.sample_controls(V, B, n, ns, 40 + i) for i in range(2)]
+    ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=16, chain=True)
+    ep.step(controls=pool[0])
+    ep.flush()
+    assert ep.chain_error() == 0
+    ep.cfg.L = 0.45                      # state reset with L = 0.5
+    ep.step(controls=pool[1])
+    ep.flush()
+    assert ep.chain_error() == 2
+
+
+@pytest.mark.parametrize("wheelbase", [0.5, 0.45])
+def test_chained_exchange_path_and_graph_capture(engine, wheelbase):
     """The chained multi-GPU step (launch: rollout of step k + selection over
     step k-1's gathered winners; then step k's local finalize and the RCCL
     all_gather) over a 1-rank nccl group, eager and graph-captured, logs the
-    steps of the single-GPU episode."""
+    steps of the single-GPU episode; both wheelbase forms."""
     import torch.distributed as dist
     from diplomjourney_amd import math_model_tree as mmt
     from diplomjourney_amd.episode import DeviceEpisode
@@ -468,7 +492,7 @@ def test_chained_exchange_path_and_graph_capture(engine):
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
     pool = [engine.sample_controls(V, B, n, ns, 900 + i) for i in range(steps)]
-    ref = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64)
+    ref = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64, L=wheelbase)
     for i in range(steps):
         ref.step(controls=pool[i])
     want = _episode_log(ref)
@@ -482,7 +506,7 @@ def test_chained_exchange_path_and_graph_capture(engine):
                                 world_size=1, device_id=torch.device("cuda", 0))
     try:
         ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64,
-                           exchange=True, chain=True)
+                           exchange=True, chain=True, L=wheelbase)
         half = steps // 2
         for i in range(half):
             ep.step(controls=pool[i])
