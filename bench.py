@@ -104,6 +104,10 @@ def parse():
     ap.add_argument("--no-chain", action="store_true",
                     help="separate selection launch per step instead of chained steps "
                          "(mpc_episode_chain_step: the step's launch completes the previous step)")
+    ap.add_argument("--run", action="store_true",
+                    help="persistent run: the K timed steps in ONE launch (mpc_episode_run; "
+                         "rect+cum, one GPU, resident inputs): step j+1's tiles stream while "
+                         "step j is being selected")
     ap.add_argument("--no-graph", action="store_true",
                     help="time eagerly launched steps instead of a HIP graph replay")
     ap.add_argument("--exchange", action="store_true",
@@ -218,12 +222,21 @@ def main():
                            exchange=exchange, split=not args.fused,
                            chain=not args.no_chain and args.integrator == "rect+cum")
     pool = make_pool(eng, ep, n_steps, args.steps) if inputs == "resident" else None
-    main_run = run_steps(args, ep, pool, use_graph, world, device)
-    use_graph = main_run["graph"]
-    kern_ms = main_run["kernel_in_step_ms"]
-    if hasattr(ep, "partials"):
-        kern_ms = kernel_pass(ep, pool if pool is not None else
-                              make_pool(eng, ep, n_steps, 4))
+    persistent = args.run
+    if persistent and (exchange or args.host_loop or inputs != "resident"
+                       or args.integrator != "rect+cum"):
+        raise SystemExit("--run: one GPU, resident inputs, --integrator rect+cum")
+    if persistent:
+        main_run = run_persistent(args, ep, pool, world, device)
+        use_graph = False
+        kern_ms = main_run["kernel_ms"]
+    else:
+        main_run = run_steps(args, ep, pool, use_graph, world, device)
+        use_graph = main_run["graph"]
+        kern_ms = main_run["kernel_in_step_ms"]
+        if hasattr(ep, "partials"):
+            kern_ms = kernel_pass(ep, pool if pool is not None else
+                                  make_pool(eng, ep, n_steps, 4))
     other = None
     if not args.host_loop and not args.no_second_pass:
         # the other input mode, same episode machinery, for comparison
@@ -234,7 +247,7 @@ def main():
                  "ms_per_step": r["elapsed"] / args.steps * 1e3, "p50_ms": r["p50_ms"]}
         del other_pool
     elapsed = main_run["elapsed"]
-    bytes_launch = 16.0 * n_steps * ep.n_local
+    bytes_launch = 16.0 * n_steps * ep.n_local * (args.steps if persistent else 1)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     value = n_total * args.steps / elapsed
     if not args.host_loop:
@@ -258,10 +271,16 @@ def main():
                    "integrator": args.integrator, "inputs": INPUTS_DOC[inputs],
                    "episodes_started": episodes,
                    "episode_loop": "host" if args.host_loop else "device-resident",
-                   "launch": (("hipGraph of the K steps" + (" incl. the RCCL all_gather"
+                   "launch": ("one persistent launch of the K steps (mpc_episode_run)"
+                              if persistent else
+                              (("hipGraph of the K steps" + (" incl. the RCCL all_gather"
                                                              if exchange else ""))
-                              if use_graph else "eager"),
-                   "step_launches": (("chained: rollout of step k + completion of step k-1 in "
+                               if use_graph else "eager")),
+                   "step_launches": ("persistent: units of 512 candidates claimed in order "
+                                     "across steps; block 0 selects step j (records, winner "
+                                     "re-roll, episode update) while step j+1 streams"
+                                     if persistent else
+                                     ("chained: rollout of step k + completion of step k-1 in "
                                       "one launch" + (" (+ local finalize + all_gather)"
                                                       if exchange else ""))
                                      if getattr(ep, "chain", False) and inputs == "resident"
@@ -270,9 +289,12 @@ def main():
                    "parallelism": f"candidate-sharded x{world}" + (", all_gather(808 B)/step"
                                                                    if exchange else "")},
         "p50_ms": main_run["p50_ms"], "p90_ms": main_run["p90_ms"],
-        "p50_note": "GPU time per MPC step (HIP events between step starts, eager launches)",
+        "p50_note": ("MPC-step period: device clock between consecutive step completions "
+                     "(selection published) inside the timed persistent launch" if persistent else
+                     "GPU time per MPC step (HIP events between step starts, eager launches)"),
         "kernel_ms": kern_ms, "kernel_in_step_ms": main_run["kernel_in_step_ms"],
-        "roofline": roofline(achieved, bytes_launch, args.traffic_json),
+        "roofline": roofline(achieved, bytes_launch, args.traffic_json,
+                             kernel="k_episode_run" if persistent else "k_rollout_argmin_stream"),
         "other_inputs": other,
         "cpu_baseline": cpu,
     }
@@ -394,6 +416,43 @@ def run_steps(args, ep, pool, use_graph, world, device):
             "kernel_in_step_ms": sum(a.elapsed_time(b) for a, b in kern) / len(kern)}
 
 
+def run_persistent(args, ep, pool, world, device):
+    """The K timed steps as one persistent launch (mpc_episode_run): warmup
+    launch of W steps, then the timed launch between a barrier + sync on
+    both sides.  kernel_ms = HIP events around the timed launch on its stream
+    (the run workspace's memset node + the kernel); the MPC-step period comes
+    from the device clock each step's selection writes when it publishes."""
+    import torch
+    import torch.distributed as dist
+    from diplomjourney_amd.episode import percentile
+    K, W = args.steps, args.warmup
+    batches = [pool[i % len(pool)] for i in range(K)]
+    if W:
+        ep.run([pool[i % len(pool)] for i in range(W)])
+    ep._ptr_table(batches[:ep.log_capacity])          # pointer table uploaded untimed
+    clock = torch.zeros(K, dtype=torch.int64, device=device)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record()
+    ep.run(batches, clock=clock)
+    e1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    assert ep.chain_error() == 0, "persistent run: a bounded wait timed out"
+    ticks = clock.cpu().tolist()
+    period_ms = [(b - a) * 1e-5 for a, b in zip(ticks, ticks[1:])]   # 100 MHz ticks
+    return {"elapsed": elapsed, "graph": False, "p50_ms": percentile(period_ms, 50),
+            "p90_ms": percentile(period_ms, 90), "kernel_ms": e0.elapsed_time(e1),
+            "kernel_in_step_ms": e0.elapsed_time(e1) / K}
+
+
 def kernel_pass(ep, pool, reps=100):
     """The rollout kernel alone: REPS back-to-back launches between two HIP
     events on the launch stream, rotating over the resident batches (at least
@@ -416,7 +475,7 @@ def kernel_pass(ep, pool, reps=100):
     return k0.elapsed_time(k1) / reps
 
 
-def roofline(achieved, bytes_launch, traffic_json):
+def roofline(achieved, bytes_launch, traffic_json, kernel="k_rollout_argmin_stream"):
     """traffic: HBM bytes per launch from the committed PMC summary, used only
     when it was measured on a launch of the same algorithmic size."""
     traffic, src = None, None
@@ -427,7 +486,7 @@ def roofline(achieved, bytes_launch, traffic_json):
             traffic, src = t.get("hbm_bytes_per_launch"), os.path.relpath(traffic_json, REPO)
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
-            "kernel": "k_rollout_argmin_stream", "algorithmic_bytes_per_launch": bytes_launch}
+            "kernel": kernel, "algorithmic_bytes_per_launch": bytes_launch}
 
 
 def bench_robots(args, wl, eng, rank, world, cpu):
