@@ -51,7 +51,10 @@ static_assert(kCplWide == 2 || kCplWide == 4, "MPC_CPL must be 2 or 4");
 constexpr int kPrefetch = MPC_PREFETCH;
 static_assert(kPrefetch >= 2, "MPC_PREFETCH must be >= 2");
 constexpr int kWaves = kBlock / 64;
-constexpr int64_t kMaxBlocks = 2048;  // 256 CUs x 8 resident blocks upper bound
+#ifndef MPC_MAX_BLOCKS
+#define MPC_MAX_BLOCKS 2048   // A/B probes cap the rollout grid lower
+#endif
+constexpr int64_t kMaxBlocks = MPC_MAX_BLOCKS;  // 256 CUs x 8 resident blocks upper bound
 #ifndef MPC_FIN_BLOCK
 #define MPC_FIN_BLOCK 256    // threads of the one-block finalize kernels (A/B: 1024 -> 256 = -0.7 us)
 #endif

@@ -574,6 +574,14 @@ int mpc_debug_run_stats(unsigned long long* host32) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_run_stats), z, sizeof(z)) == hipSuccess ? MPC_OK
                                                                                 : MPC_ERR_HIP;
 }
+// Debug builds only: per-unit timestamps [n_units][8] (n_units <= 1 << 20).
+int mpc_debug_run_unit_times(unsigned long long* host, int64_t n_units) {
+  if (n_units < 0 || n_units > (1 << 20)) return MPC_ERR_ARG;
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpyFromSymbol(host, HIP_SYMBOL(g_run_ut), n_units * 8 * 8) != hipSuccess)
+    return MPC_ERR_HIP;
+  return MPC_OK;
+}
 // Debug builds only: the per-step timeline [512][5], then reset (min fields to ~0).
 int mpc_debug_run_timeline(unsigned long long* host2560) {
   if (hipDeviceSynchronize() != hipSuccess ||

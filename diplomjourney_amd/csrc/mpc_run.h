@@ -60,6 +60,15 @@ __device__ unsigned long long g_run_stats[32];
 #define RUN_STAT(i, v) atomicAdd(&g_run_stats[i], static_cast<unsigned long long>(v))
 #define RUN_TICK() __builtin_amdgcn_s_memrealtime()
 #define RUN_ACC(i, v) (st_acc[i] += static_cast<uint64_t>(v))
+// per-unit timestamps (units < 1 << 20): 0 stream start, 1 stream end, 2
+// parked, 3 completed, 4 ticks the streaming wave 0 waited for this unit's
+// claim, 5 completer: quarters parked and head known (completion start),
+// 6 claim issued (plain stores by lane 0 of wave 0 / the completer)
+__device__ unsigned long long g_run_ut[1 << 20][8];
+#define RUN_UT(u, f) \
+  do { if ((u) < (1 << 20)) g_run_ut[(u)][(f)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define RUN_UTV(u, f, v) \
+  do { if ((u) < (1 << 20)) g_run_ut[(u)][(f)] = (v); } while (0)
 // per-step timeline (steps < 512): 0 first unit stream start (min), 1 last
 // stream end (max), 2 last unit completion (max), 3 sweep done, 4 published
 __device__ unsigned long long g_run_tl[512][5];
@@ -70,6 +79,8 @@ __device__ unsigned long long g_run_tl[512][5];
 #else
 #define RUN_TL_MIN(j, f) ((void)0)
 #define RUN_TL_MAX(j, f) ((void)0)
+#define RUN_UT(u, f) ((void)0)
+#define RUN_UTV(u, f, v) ((void)0)
 #define RUN_STAT(i, v) ((void)0)
 #define RUN_TICK() 0ull
 #define RUN_ACC(i, v) ((void)0)
@@ -82,8 +93,9 @@ constexpr uint32_t kRunSpinLimit = 1u << 18;   // x s_sleep(16) ~1 us: ~0.25 s
 struct RunCtl {
   uint32_t abort;        // a bounded wait timed out: every wait gives up
   uint32_t claim;        // next unit to hand out (claimed by the completer waves)
-  uint32_t role;         // blocks started: the first one selects
-  uint32_t pad_[29];
+  uint32_t role;         // blocks registered (in start order): the first one selects
+  uint32_t nres;         // registered blocks when the selector closed the registration
+  uint32_t pad_[28];
   uint64_t pub[2][kHeadDwords];   // head of step j in pub[j & 1], tag j + 1
 };
 static_assert(sizeof(RunCtl) % 16 == 0, "memset block: multiple of 16 B");
@@ -136,6 +148,41 @@ __device__ __forceinline__ double run_words_t(const uint32_t* s_w) {
   const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(s_w[kRunTDword]));
   const uint64_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(s_w[kRunTDword + 1]));
   return __longlong_as_double(static_cast<long long>((hi << 32) | lo));
+}
+
+// Consts from head granules (data in the high 32 bits), field by field.
+__device__ __forceinline__ Consts consts_from_granules(const uint64_t* g) {
+  auto d = [&](size_t off) {
+    const int q = static_cast<int>(off / 4);
+    const uint64_t lo = static_cast<uint32_t>(
+        __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(g[q] >> 32)));
+    const uint64_t hi = static_cast<uint32_t>(
+        __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(g[q + 1] >> 32)));
+    return __longlong_as_double(static_cast<long long>((hi << 32) | lo));
+  };
+  Consts K;
+  K.x = d(offsetof(Consts, x));
+  K.y = d(offsetof(Consts, y));
+  K.phi = d(offsetof(Consts, phi));
+  K.x_t = d(offsetof(Consts, x_t));
+  K.y_t = d(offsetof(Consts, y_t));
+  K.x_0 = d(offsetof(Consts, x_0));
+  K.y_0 = d(offsetof(Consts, y_0));
+  K.A = d(offsetof(Consts, A));
+  K.B = d(offsetof(Consts, B));
+  K.C1 = d(offsetof(Consts, C1));
+  K.C2 = d(offsetof(Consts, C2));
+  K.den = d(offsetof(Consts, den));
+  K.L = d(offsetof(Consts, L));
+  K.inv_L = d(offsetof(Consts, inv_L));
+  K.h = d(offsetof(Consts, h));
+  K.hlgth = d(offsetof(Consts, hlgth));
+  K.s0 = d(offsetof(Consts, s0));
+  K.c0 = d(offsetof(Consts, c0));
+  K.L_pow2 = static_cast<int32_t>(__builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(g[offsetof(Consts, L_pow2) / 4] >> 32)));
+  K.pad_ = 0;
+  return K;
 }
 
 // Step j's T unit records (kRunRecWords granules each, tag j + 1) -> the
@@ -205,9 +252,6 @@ __device__ __forceinline__ void run_sweep_records(const uint64_t* rec, int64_t T
   }
 }
 
-#ifndef MPC_RUN_WAVES
-#define MPC_RUN_WAVES 4   // launch bound of the run kernel (A/B: tools/build_variant.sh)
-#endif
 
 // Block 0 of the run: completes the K steps one after the other.  Step j:
 // sweep its T unit records (tag j + 1), re-roll the winner, episode update,
@@ -272,26 +316,53 @@ __device__ __noinline__ void run_select_step(
   __syncthreads();   // s_log / s_slot reuse
 }
 
-// Per streaming block: the parking slot (one unit: 4 waves x 64 lanes x two
-// candidates' position sums and irregular flags, the h each wave's loop used)
-// and the completer's knowledge of the heads (read by the streaming waves
-// for the speculation).  LDS only; streaming waves and the completer order
+// Per streaming block: the parking slots (one unit each: 4 waves x 64 lanes x
+// two candidates' position sums and irregular flags, the h each wave's loop
+// used) and the quarter minima.  LDS only; the four streaming waves order
 // their accesses with lgkmcnt waits (LDS operations of a wave complete in
 // order) and relaxed LDS atomics.
+#ifndef MPC_RUN_SLOTS
+#define MPC_RUN_SLOTS 2
+#endif
+constexpr int kRunSlots = MPC_RUN_SLOTS;   // parking slots per block (unit k in slot k % kRunSlots)
+static_assert(kRunSlots >= 1 && kRunSlots <= 8, "MPC_RUN_SLOTS must be in [1, 8]");
+// The run's own control ring (kRunRing - 1 steps in flight per wave).  (4
+// slots: 54272 B of LDS a block, and only 2 blocks per CU became resident.)
+#ifndef MPC_RUN_RING
+#define MPC_RUN_RING 3
+#endif
+constexpr int kRunRing = MPC_RUN_RING;
+static_assert(kRunRing >= 2 && kRunRing <= 4, "MPC_RUN_RING must be in [2, 4]");
+__shared__ double2 g_run_ring[kWaves][kRunRing][2][64];  // [wave][slot][v|beta][lane]
 struct RunLds {
-  double2 px[kBlock], py[kBlock];   // per streaming lane: (A0, A1), (B0, B1)
-  uint32_t bad[kBlock];             // bit c: candidate c irregular
-  double ph[kWaves];                // h of each wave's loop
-  int32_t cnt;                      // quarters parked in the slot
-  int32_t seq;                      // unit index (per block) the slot accepts next
-  int32_t jknown;                   // latest step whose head the completer took
-  int32_t qn;                       // units claimed for this block so far
-  int64_t q[4];                     // unit claimed as the block's k-th in q[k & 3]
-  double tring[8];                  // t of step jknown in tring[jknown & 7]
-  uint32_t hw[64];                  // the completer's head words (loop words)
+  double2 px[kRunSlots][kBlock], py[kRunSlots][kBlock];   // per streaming lane: (A0,A1), (B0,B1)
+  uint64_t badm[kRunSlots][kWaves][2];   // ballot of candidate c irregular, per wave
+  double ph[kRunSlots][kWaves];     // h of each wave's loop
+  uint64_t qkey[kRunSlots][kWaves]; // each wave's quarter minimum
+  int64_t qidx[kRunSlots][kWaves];
+  int32_t cnt[kRunSlots];           // quarters of the slot's unit scored
+  int32_t seq[kRunSlots];           // unit index (per block) the slot accepts next
+  uint64_t poll[kWaves][64];        // each wave's head poll (LDS-DMA target)
 };
 
 __device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// 16 bytes (two granules) of a published head into this lane's 16 bytes of
+// the LDS buffer at dst (lanes 0-31: 64 granules), bypassing the non-coherent
+// cache levels (sc1, as an agent-scope relaxed load).  Counted by vmcnt like
+// the control rows; the caller orders earlier LDS reads of the buffer first.
+__device__ __forceinline__ void glds_poll(const uint64_t* g, uint32_t dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off sc1\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(dst)
+      : "memory");
+}
 
 __device__ __forceinline__ int32_t lds_load(const int32_t* p) {
   return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED,
@@ -301,37 +372,90 @@ __device__ __forceinline__ void lds_store(int32_t* p, int32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Streaming wave (waves 0-3 of blocks 1..): rolls out its quarter (128
+// One wave: the unit's four quarter minima (LDS) -> unit u's record (step j,
+// tag j + 1); then the slot is free for the block's unit k + kRunSlots.
+__device__ __forceinline__ void run_combine(RunLds& sh, uint64_t* __restrict__ rec, int64_t T,
+                                            int sl, int32_t k, int64_t u, int64_t j) {
+  const int lane = threadIdx.x & 63;
+  uint64_t bk = ~0ull;
+  int64_t bi = INT64_MAX;
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) {
+    const uint64_t k2 = sh.qkey[sl][w];
+    const int64_t i2 = sh.qidx[sl][w];
+    if (rec_less(k2, i2, bk, bi)) {
+      bk = k2;
+      bi = i2;
+    }
+  }
+  if (lane == 0) {
+    const uint32_t tag = static_cast<uint32_t>(j + 1);
+    uint64_t* r = rec + ((j & 1) * T + (u - j * T)) * kRunRecWords;
+    granule_store(r, tag, static_cast<uint32_t>(bk >> 32));
+    granule_store(r + 1, tag, static_cast<uint32_t>(bk));
+    granule_store(r + 2, tag, static_cast<uint32_t>(bi));   // < 2^31 (host check)
+    RUN_UT(u, 3);
+    lds_store(&sh.cnt[sl], 0);
+    lds_order();
+    lds_store(&sh.seq[sl], k + kRunSlots);
+  }
+}
+
+// The rare path of scoring a parked candidate (out of line: it must not cost
+// the streaming loop registers): a mis-speculated step size (an episode
+// restart reset t) re-rolls the candidate from its controls with the head's
+// h; an irregular candidate re-runs the safe recurrence; otherwise the
+// parked sums give the pose.  `head`: the step's head granules (LDS).
+template <int INTEG, bool PL2>
+__device__ __noinline__ uint64_t run_rescore(const uint64_t* head, double hq, const double* cv,
+                                             const double* cb, int64_t n_cand, int n_steps,
+                                             int64_t col, double a, double b, bool irregular) {
+  const Consts K = consts_from_granules(head);
+  double cst;
+  if (hq != K.h) {
+    cst = rollout_candidate_l<INTEG, kRotCum, PL2>(K, cv, cb, n_cand, col, n_steps, nullptr);
+  } else if (irregular) {
+    double xx = K.x, yy = K.y, ph = K.phi;
+    for (int sr = 0; sr < n_steps; ++sr)
+      step_safe<INTEG>(xx, yy, ph, cv[sr * n_cand + col], cb[sr * n_cand + col], K);
+    cst = cost(xx, yy, K);
+  } else {
+    double xx, yy;
+    cum_pose(K, a, b, xx, yy);
+    cst = cost(xx, yy, K);
+  }
+  return cost_key(cst);
+}
+
+// Streaming wave (waves 0-3 of a streaming block): rolls out its quarter (128
 // candidates: lane l of wave w holds candidates tile*512 + (64w + l)*2 + {0,1})
-// of each of the block's units and parks the sums.  The control ring (kRing
-// slots of one step's v and beta rows, kRing-1 steps in flight) continues
-// across units; the only waits are the counted vmcnt waits of its own rows
-// and, before parking, for the parking slot to be free.
+// of each of the block's units (s, s + G, s + 2G, ... for streaming block s of
+// G), parks the sums and goes on.  The control ring (kRing slots of one step's
+// v and beta rows, kRing-1 steps in flight) continues across units.  The
+// wave learns a parked quarter's head by polling it with an LDS-DMA into its
+// own buffer (it lands behind the counted waits two steps later), scores the
+// quarter and counts it; the wave whose count completes the unit combines the
+// four minima into the unit's record and frees the slot.  The only blocking
+// waits: its own control rows, and at a unit's end, when all kRunSlots slots
+// hold this wave's unscored quarters, the oldest one's head.
 template <int INTEG, bool PL2>
 __device__ __forceinline__ void run_stream_wave(RunLds& sh, const double* const* __restrict__ ctl,
-                                                int64_t total, int64_t T, int64_t n_cand,
-                                                int n_steps, RunCtl* __restrict__ rc,
+                                                int64_t total, int64_t T, int64_t s, int64_t G,
+                                                int64_t n_cand, int n_steps,
+                                                RunCtl* __restrict__ rc,
+                                                uint64_t* __restrict__ rec,
                                                 EpisodeState* __restrict__ S, const Consts& Kc,
                                                 double delta_t) {
   constexpr int CPL = 2;
-  constexpr int R = kRing;
+  constexpr int R = kRunRing;
   constexpr uint32_t kSlot = 2 * 64 * sizeof(double2);   // 2 KiB: v and beta rows
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t ring0 = __builtin_amdgcn_readfirstlane(lds_addr(&g_ring[wv][0][0][0]));
+  const uint32_t ring0 = __builtin_amdgcn_readfirstlane(lds_addr(&g_run_ring[wv][0][0][0]));
   auto dst = [&](uint32_t slot) { return ring0 + slot * kSlot; };
-  // the block's k-th unit, from the completer's claims (normally long there)
-  auto unit_of = [&](int32_t k) -> int64_t {
-    for (uint32_t it = 0; lds_load(&sh.qn) <= k; ++it) {
-      if ((it & 1023) == 1023 && run_aborted(rc)) return total;
-      if (it >= kRunSpinLimit * 8u) {
-        if (lane == 0) run_fail(rc, S, 5);
-        return total;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    lds_order();
-    return sh.q[k & 3];
+  auto unit_of = [&](int32_t k) -> int64_t {   // the block's k-th unit
+    const int64_t u = s + static_cast<int64_t>(k) * G;
+    return u < total ? u : total;
   };
   auto lane_col = [&](int64_t tile) {
     const int64_t c0 = tile * (kBlock * CPL) + threadIdx.x * CPL;
@@ -380,13 +504,131 @@ __device__ __forceinline__ void run_stream_wave(RunLds& sh, const double* const*
 #ifdef MPC_RUN_STATS
   uint64_t st_acc[16] = {0};
 #endif
+  // This wave's parked, unscored quarters: units pk0 .. pk0 + pend_n - 1 of
+  // the block (consecutive; sums in slot k % kRunSlots, speculated h in
+  // sh.ph[slot][wv]).
+  const uint32_t pollw = __builtin_amdgcn_readfirstlane(lds_addr(&sh.poll[wv][0]));
+  int pend_n = 0;
+  int32_t pk0 = 0;                       // oldest pending unit of the block
+  int64_t pj0 = 0;                       // its step
+  int64_t khj = 0;                       // latest step whose head this wave took (poll buffer)
+  double kt = S->h.t;                    // that head's t (the speculation's base)
+  int poll_age = 0;                      // 0: none in flight; else steps waited since issue
+  int64_t poll_j = 0;
+  {
+    // the call's first head, as if polled (tag 1 = step 0)
+    const int q = lane;
+    const uint32_t w = run_loop_word(q) ? reinterpret_cast<const uint32_t*>(&S->h)[q] : 0u;
+    sh.poll[wv][q] = (static_cast<uint64_t>(w) << 32) | 1u;
+  }
+  auto head_t = [&]() {
+    const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(sh.poll[wv][kRunTDword] >> 32)));
+    const uint64_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(sh.poll[wv][kRunTDword + 1] >> 32)));
+    return __longlong_as_double(static_cast<long long>((hi << 32) | lo));
+  };
+  // score the oldest pending quarter with the head in the poll buffer (step pj0)
+  auto resolve_oldest = [&]() {
+    const int sl = pk0 % kRunSlots;
+    const int64_t u0 = unit_of(pk0);
+    const double ph0 = sh.ph[sl][wv];
+    const double tj = head_t();
+    const bool hok = ((tj + delta_t) - tj) == ph0;
+    const uint32_t bb = static_cast<uint32_t>((sh.badm[sl][wv][0] >> lane) & 1u) |
+                        (static_cast<uint32_t>((sh.badm[sl][wv][1] >> lane) & 1u) << 1);
+    const double2 px = sh.px[sl][threadIdx.x], py = sh.py[sl][threadIdx.x];
+    const int64_t c0 = (u0 - pj0 * T) * (kBlock * CPL) + threadIdx.x * CPL;
+    uint64_t k0, k1;
+    if (hok && __ballot(bb != 0u) == 0) {
+      const Consts K = consts_from_granules(sh.poll[wv]);
+      double xx, yy;
+      cum_pose(K, px.x, py.x, xx, yy);
+      k0 = cost_key(cost(xx, yy, K));
+      cum_pose(K, px.y, py.y, xx, yy);
+      k1 = cost_key(cost(xx, yy, K));
+    } else {
+      RUN_ACC(1, 1);
+      const int64_t cl = c0 < n_cand ? c0 : n_cand - CPL;
+      const double* cv = ctl[2 * pj0];
+      const double* cb = ctl[2 * pj0 + 1];
+      k0 = run_rescore<INTEG, PL2>(sh.poll[wv], ph0, cv, cb, n_cand, n_steps, cl, px.x, py.x,
+                                   (bb & 1u) != 0u);
+      k1 = run_rescore<INTEG, PL2>(sh.poll[wv], ph0, cv, cb, n_cand, n_steps, cl + 1, px.y, py.y,
+                                   (bb & 2u) != 0u);
+    }
+    uint64_t dk = ~0ull;
+    int64_t di = INT64_MAX;
+    if (c0 < n_cand) {
+      dk = k0;
+      di = c0;
+    }
+    if (c0 + 1 < n_cand && k1 < dk) {
+      dk = k1;
+      di = c0 + 1;
+    }
+    wave_argmin(dk, di);
+    if (lane == 0) {
+      sh.qkey[sl][wv] = dk;
+      sh.qidx[sl][wv] = di;
+    }
+    lds_order();   // the minimum is in LDS before the count says so
+    int32_t prev = 0;
+    if (lane == 0)
+      prev = __hip_atomic_fetch_add(&sh.cnt[sl], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev == kWaves - 1) {
+      lds_order();
+      run_combine(sh, rec, T, sl, pk0, u0, pj0);
+    }
+    ++pk0;
+    if (--pend_n > 0) pj0 = unit_of(pk0) / T;
+  };
+  // after a poll has landed: take it if every loop word carries the tag
+  auto take_poll = [&]() {
+    const int q = lane;
+    const uint64_t w = sh.poll[wv][q];
+    const bool ok =
+        !run_loop_word(q) || static_cast<uint32_t>(w) == static_cast<uint32_t>(poll_j + 1);
+    if (__ballot(!ok) == 0) {
+      khj = poll_j;
+      kt = head_t();
+    }
+    poll_age = 0;
+    while (pend_n > 0 && khj == pj0) resolve_oldest();
+  };
+  // blocking: the head of the oldest pending quarter (relaxed polls)
+  auto wait_oldest = [&]() {
+    const uint64_t* g = rc->pub[pj0 & 1];
+    const uint32_t tag = static_cast<uint32_t>(pj0 + 1);
+    const uint64_t w0 = RUN_TICK();
+    for (uint32_t it = 0;; ++it) {
+      const uint64_t w = run_loop_word(lane) ? granule_load(g + lane) : 0ull;
+      const bool ok = !run_loop_word(lane) || static_cast<uint32_t>(w) == tag;
+      if (__ballot(!ok) == 0) {
+        sh.poll[wv][lane] = w;
+        break;
+      }
+      if (it >= kRunSpinLimit || run_aborted(rc)) {
+        if (lane == 0) run_fail(rc, S, 2);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+    lds_order();
+    khj = pj0;
+    kt = head_t();
+    poll_age = 0;
+    RUN_ACC(5, 1);
+    RUN_ACC(6, RUN_TICK() - w0);
+    while (pend_n > 0 && khj == pj0) resolve_oldest();
+  };
   for (int32_t k = 0; u < total; ++k, u = unit_of(k)) {
     const int64_t j = u / T;
-    // step size: from the completer's latest head, + dt per step since
+    // step size: from this wave's latest head, + dt per step since
     {
-      const int32_t jk = lds_load(&sh.jknown);
-      double t = sh.tring[jk & 7];
-      for (int64_t q = jk; q < j; ++q) t = t + delta_t;
+      double t = kt;
+      for (int64_t q = khj; q < j; ++q) t = t + delta_t;
       Kl.h = (t + delta_t) - t;          // consts_from_problem: t_b - t_a
     }
     double x[CPL], y[CPL], sn[CPL], cs[CPL];
@@ -397,47 +639,81 @@ __device__ __forceinline__ void run_stream_wave(RunLds& sh, const double* const*
       step_start<kRotCum>(Kl, x[q], y[q], ph, sn[q], cs[q]);
       bad[q] = false;
     }
-    if (lane == 0) RUN_TL_MIN(j, 0);
+    if (lane == 0 && wv == 0) {
+      RUN_UT(u, 0);
+      RUN_UTV(u, 7, blockIdx.x);
+    }
 #pragma unroll 1
     for (int st = 0; st < n_steps; ++st) {
       issue(true, rv, rb);
-      const uint32_t ahead = gi - gc - 1;   // rows in flight behind this one
-      if (ahead >= 2)
+      const uint32_t ahead = gi - gc - 1;   // row pairs issued behind this one
+      static_assert(R <= 4, "tail waits below cover up to 3 pairs behind");
+      if (ahead >= R - 1)
         wait_vm<2 * (R - 1)>();
+      else if (ahead == 2)
+        wait_vm<4>();
       else if (ahead == 1)
         wait_vm<2>();
       else
         wait_vm<0>();
       const uint32_t sl = gc % R;
-      rv = g_ring[wv][sl][0][lane];
-      rb = g_ring[wv][sl][1][lane];
+      rv = g_run_ring[wv][sl][0][lane];
+      rb = g_run_ring[wv][sl][1][lane];
       ++gc;
       // (the heading itself is not carried: kRotCum rotates (sn, cs))
-      double ph0 = 0.0, ph1 = 0.0;
-      step_core<INTEG, kRotCum, PL2>(x[0], y[0], ph0, sn[0], cs[0], rv.x, rb.x, Kl, bad[0], &lead);
-      step_core<INTEG, kRotCum, PL2>(x[1], y[1], ph1, sn[1], cs[1], rv.y, rb.y, Kl, bad[1], &lead);
+      double h0 = 0.0, h1 = 0.0;
+      step_core<INTEG, kRotCum, PL2>(x[0], y[0], h0, sn[0], cs[0], rv.x, rb.x, Kl, bad[0], &lead);
+      step_core<INTEG, kRotCum, PL2>(x[1], y[1], h1, sn[1], cs[1], rv.y, rb.y, Kl, bad[1], &lead);
+      // the head poll of the oldest pending quarter: issued here, landed R-1
+      // counted waits later (R-1 more row pairs issued behind it), then taken
+      if (poll_age > 0 && ++poll_age >= R) take_poll();
+      if (pend_n > 0 && poll_age == 0) {
+        poll_j = pj0;
+        lds_order();   // this wave's reads of the previous poll are done
+        if (lane < 32) glds_poll(rc->pub[pj0 & 1] + 2 * lane, pollw);
+        poll_age = 1;
+      }
     }
-    if (lane == 0) RUN_TL_MAX(j, 1);
-    // park: wait for the slot (the completer frees it after the previous unit)
+    if (lane == 0 && wv == 0) RUN_UT(u, 1);
+    // the slot of unit k held unit k - kRunSlots: if that one is still this
+    // wave's to score, wait for its head; then wait until the unit is combined
+    const int sl = k % kRunSlots;
+    if (pend_n == kRunSlots) {
+      if (poll_age > 0) wait_vm<0>();    // (an in-flight poll must land first)
+      poll_age = 0;
+      wait_oldest();
+    }
     const uint64_t p0t = RUN_TICK();
-    if (lds_load(&sh.seq) != k) RUN_ACC(5, 1);
-    for (uint32_t it = 0; lds_load(&sh.seq) != k; ++it) {
+    for (uint32_t it = 0; lds_load(&sh.seq[sl]) != k; ++it) {
       if ((it & 1023) == 1023 && run_aborted(rc)) break;
       if (it >= kRunSpinLimit * 8u) {
-        if (lane == 0) run_fail(rc, S, 2);
+        if (lane == 0) run_fail(rc, S, 4);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
     RUN_ACC(4, RUN_TICK() - p0t);
-    sh.px[threadIdx.x] = make_double2(x[0], x[1]);
-    sh.py[threadIdx.x] = make_double2(y[0], y[1]);
-    sh.bad[threadIdx.x] = (bad[0] ? 1u : 0u) | (bad[1] ? 2u : 0u);
-    if (lane == 0) sh.ph[wv] = Kl.h;
-    lds_order();   // the quarter's words are in LDS before the count says so
-    if (lane == 0)
-      __hip_atomic_fetch_add(&sh.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0 && wv == 0) RUN_UT(u, 2);
+    sh.px[sl][threadIdx.x] = make_double2(x[0], x[1]);
+    sh.py[sl][threadIdx.x] = make_double2(y[0], y[1]);
+    {
+      const uint64_t b0 = __ballot(bad[0]), b1 = __ballot(bad[1]);
+      if (lane == 0) {
+        sh.badm[sl][wv][0] = b0;
+        sh.badm[sl][wv][1] = b1;
+        sh.ph[sl][wv] = Kl.h;
+      }
+    }
+    if (pend_n++ == 0) {
+      pk0 = k;
+      pj0 = j;
+    }
+    lds_order();
+    // this wave already holds the head of its oldest pending step: score now
+    while (pend_n > 0 && khj == pj0) resolve_oldest();
   }
+  if (poll_age > 0) wait_vm<0>();
+  while (pend_n > 0) wait_oldest();   // the wave's last quarters
 #ifdef MPC_RUN_STATS
   if (lane == 0)
     for (int q = 0; q < 16; ++q)
@@ -445,153 +721,26 @@ __device__ __forceinline__ void run_stream_wave(RunLds& sh, const double* const*
 #endif
 }
 
-// Completer wave (wave 4 of blocks 1..): for each unit of the block, once its
-// four quarters are parked and step j's head is published: criteria, the
-// unit's (cost, index) minimum, one tagged record; then frees the slot.
-template <int INTEG, bool PL2>
-__device__ __forceinline__ void run_complete_wave(RunLds& sh, const double* const* __restrict__ ctl,
-                                                  int64_t total, int64_t T, int64_t n_cand,
-                                                  int n_steps, RunCtl* __restrict__ rc,
-                                                  uint64_t* __restrict__ rec,
-                                                  EpisodeState* __restrict__ S) {
-  constexpr int CPL = 2;
-  const int lane = threadIdx.x & 63;
-  int64_t jk = 0;
-#ifdef MPC_RUN_STATS
-  uint64_t st_acc[16] = {0};
-#endif
-  // claims: units are handed out in increasing order to running blocks only,
-  // so the lowest unselected unit's block can always go on; this block's k-th
-  // unit is claimed when it starts completing its (k-2)-th
-  auto claim = [&](int32_t k) {
-    if (lane == 0) {
-      const uint32_t c =
-          __hip_atomic_fetch_add(&rc->claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      sh.q[k & 3] = static_cast<int64_t>(c);
-      lds_order();
-      lds_store(&sh.qn, k + 1);
-    }
-  };
-  claim(0);
-  claim(1);
-  for (int32_t k = 0;; ++k) {
-    claim(k + 2);
-    lds_order();
-    const int64_t u = sh.q[k & 3];
-    if (u >= total) break;
-    const int64_t j = u / T;
-    const int64_t tile = u - j * T;
-    // all four quarters parked
-    const uint64_t c0t = RUN_TICK();
-    for (uint32_t it = 0; lds_load(&sh.cnt) != kWaves; ++it) {
-      if ((it & 1023) == 1023 && run_aborted(rc)) break;
-      if (it >= kRunSpinLimit * 8u) {
-        if (lane == 0) run_fail(rc, S, 3);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    lds_order();
-    const uint64_t c1t = RUN_TICK();
-    RUN_ACC(2, c1t - c0t);
-    // step j's head
-#ifdef MPC_RUN_NODEP
-    if (false) {   // A/B probe only: no dependency on the selection (results invalid)
-#else
-    if (j != jk) {
-#endif
-      const uint64_t* g = rc->pub[j & 1];
-      const uint32_t tag = static_cast<uint32_t>(j + 1);
-      for (uint32_t it = 0; !run_read_words(g, tag, sh.hw); ++it) {
-        if (it >= kRunSpinLimit || run_aborted(rc)) {
-          if (lane == 0) run_fail(rc, S, 4);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(4);
-      }
-      lds_order();
-      if (lane == 0) sh.tring[j & 7] = run_words_t(sh.hw);
-      lds_order();   // t before the step index that points at it
-      if (lane == 0) lds_store(&sh.jknown, static_cast<int32_t>(j));
-      jk = j;
-      RUN_ACC(1, 1);
-      RUN_ACC(3, RUN_TICK() - c1t);
-    }
-    RUN_ACC(0, 1);
-    const Consts K = consts_from_words(sh.hw);
-    const double* cv = ctl[2 * j];
-    const double* cb = ctl[2 * j + 1];
-    uint64_t best_k = ~0ull;
-    int64_t best_i = INT64_MAX;
-#pragma unroll 1
-    for (int w = 0; w < kWaves; ++w) {
-      const int tq = w * 64 + lane;
-      const double2 px = sh.px[tq], py = sh.py[tq];
-      const uint32_t bb = sh.bad[tq];
-      const double hq = sh.ph[w];
-      const int64_t c0 = tile * (kBlock * CPL) + tq * CPL;
-      const int64_t cl = c0 < n_cand ? c0 : n_cand - CPL;
-      const double ax[CPL] = {px.x, px.y}, ay[CPL] = {py.x, py.y};
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        double cst;
-#ifdef MPC_RUN_NODEP
-        if (false) {
-#else
-        if (hq != K.h) {   // mis-speculated step size (an episode restart reset t)
-#endif
-          cst = rollout_candidate_l<INTEG, kRotCum, PL2>(K, cv, cb, n_cand, cl + c, n_steps,
-                                                         nullptr);
-        } else if (bb & (1u << c)) {   // irregular candidate: the safe recurrence
-          double xx = K.x, yy = K.y, ph = K.phi;
-          for (int sr = 0; sr < n_steps; ++sr)
-            step_safe<INTEG>(xx, yy, ph, cv[sr * n_cand + cl + c], cb[sr * n_cand + cl + c], K);
-          cst = cost(xx, yy, K);
-        } else {
-          double xx, yy;
-          cum_pose(K, ax[c], ay[c], xx, yy);
-          cst = cost(xx, yy, K);
-        }
-        const uint64_t kk = cost_key(cst);
-        if (c0 + c < n_cand && rec_less(kk, c0 + c, best_k, best_i)) {
-          best_k = kk;
-          best_i = c0 + c;
-        }
-      }
-    }
-    wave_argmin(best_k, best_i);
-    if (lane == 0) {
-      const uint32_t tag = static_cast<uint32_t>(j + 1);
-      uint64_t* r = rec + ((j & 1) * T + tile) * kRunRecWords;
-      granule_store(r, tag, static_cast<uint32_t>(best_k >> 32));
-      granule_store(r + 1, tag, static_cast<uint32_t>(best_k));
-      granule_store(r + 2, tag, static_cast<uint32_t>(best_i));   // < 2^31 (host check)
-      RUN_TL_MAX(j, 2);
-    }
-    // free the slot: its words are read (lgkmcnt) before the next unit may write
-    lds_order();
-    if (lane == 0) {
-      lds_store(&sh.cnt, 0);
-      lds_order();
-      lds_store(&sh.seq, k + 1);
-    }
-  }
-#ifdef MPC_RUN_STATS
-  if (lane == 0)
-    for (int q = 0; q < 16; ++q)
-      if (st_acc[q]) RUN_STAT(q, st_acc[q]);
-#endif
-}
-
-constexpr int kRunThreads = kBlock + 64;   // 4 streaming waves + the completer
+constexpr int kRunThreads = kBlock;   // 4 waves: the selector's, or a streaming block's
+// Launch bound: waves per SIMD.  LDS (~46 KB a block) allows 3 blocks of 4
+// waves per CU; asking for more than LDS allows makes the bound void for the
+// out-of-line callees (run_rescore then took 180 VGPRs: 2 blocks per CU).
 #ifndef MPC_RUN_WAVES
-#define MPC_RUN_WAVES 5   // waves per SIMD: 4 blocks of 5 waves per CU
+#define MPC_RUN_WAVES 3
 #endif
+constexpr uint32_t kRunRegisterTicks = 2000;   // s_memrealtime (100 MHz): 20 us
 
 // ctl: device array [k_steps][2] of the steps' control SoA pointers (v, beta).
 // rec: [2][T][kRunRecWords] record granules (step j in half j & 1).
 // out: step k_steps-1's winner; every other step's re-roll goes to scratch.
 // clock: optional [k_steps] s_memrealtime (100 MHz) when step j was completed.
+//
+// Roles: blocks register in start order (rc->role).  The first one selects;
+// it closes the registration when every block of the grid is in, or 20 us
+// after it started with at least one other block in, and publishes the count
+// N (rc->nres).  Blocks 1 .. N-1 stream units s, s + G, ... (s = role - 1,
+// G = N - 1): every block with a unit is running, whatever the residency the
+// occupancy API promised.  A block that registers later has no unit.
 template <int INTEG, bool PL2>
 __global__ __launch_bounds__(kRunThreads, MPC_RUN_WAVES) void k_episode_run(
     EpisodeState* __restrict__ S, const double* const* __restrict__ ctl, int k_steps,
@@ -602,33 +751,50 @@ __global__ __launch_bounds__(kRunThreads, MPC_RUN_WAVES) void k_episode_run(
   constexpr int CPL = 2;
   const int64_t T = (n_cand + kBlock * CPL - 1) / (kBlock * CPL);
   const int64_t total = T * k_steps;
-  const int wv = threadIdx.x >> 6;
-  // Roles: the first block to start selects (so the selector is a running
-  // block whatever the dispatch order); the others stream and complete.
   __shared__ RunLds sh;
-  __shared__ uint32_t s_role;
-  if (threadIdx.x == 0)
-    s_role = __hip_atomic_fetch_add(&rc->role, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (wv == kWaves) {   // the head of the call's first step (S->h, written before the launch)
-    const int q = threadIdx.x & 63;
-    if (run_loop_word(q)) sh.hw[q] = reinterpret_cast<const uint32_t*>(&S->h)[q];
-    if (q == 0) {
-      sh.tring[0] = S->h.t;
-      sh.jknown = 0;
-      sh.cnt = 0;
-      sh.seq = 0;
-      sh.qn = 0;
+  __shared__ uint32_t s_role, s_nres;
+  if (threadIdx.x == 0) {
+    const uint32_t r =
+        __hip_atomic_fetch_add(&rc->role, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t n = 0;
+    if (r == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        n = __hip_atomic_load(&rc->role, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t dt = __builtin_amdgcn_s_memrealtime() - t0;
+        if (n >= gridDim.x || (n >= 2 && dt > kRunRegisterTicks) || dt > 1000 * kRunRegisterTicks)
+          break;
+        __builtin_amdgcn_s_sleep(8);
+      }
+      __hip_atomic_store(&rc->nres, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (n < 2) run_fail(rc, S, 6);   // no streaming block in 20 ms
+    } else {
+      for (uint32_t it = 0;; ++it) {
+        n = __hip_atomic_load(&rc->nres, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n != 0u || run_aborted(rc)) break;
+        if (it >= kRunSpinLimit) {
+          run_fail(rc, S, 7);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+      }
     }
+    s_role = r;
+    s_nres = n;
+  }
+  if (threadIdx.x < kRunSlots) {
+    sh.cnt[threadIdx.x] = 0;
+    sh.seq[threadIdx.x] = threadIdx.x;
   }
   __syncthreads();   // the only barrier of a streaming block
-  if (s_role == 0u) {
-    // the selector runs on waves 0-3; a wave that has ended no longer counts
-    // at the block's barriers
-    if (wv >= kWaves) return;
+  const uint32_t role = s_role, nres = s_nres;
+  if (role == 0u) {
+    if (nres < 2u) return;
     // The host picked PL2 from cfg; a state reset with another wheelbase form
     // would be rolled out with the wrong dphi form: flag it (as the chain does).
     if (threadIdx.x == 0 && (S->h.K.L_pow2 != 0) != PL2) S->chain_error = 2u;
     if (threadIdx.x == 0) g_run_cfg = ecfg;
+    if (threadIdx.x == 0) RUN_STAT(31, nres);
     if (threadIdx.x < kHeadDwords)
       g_run_head[threadIdx.x] = reinterpret_cast<const uint32_t*>(&S->h)[threadIdx.x];
     __syncthreads();
@@ -638,12 +804,11 @@ __global__ __launch_bounds__(kRunThreads, MPC_RUN_WAVES) void k_episode_run(
                              clock);
     return;
   }
-  if (wv < kWaves) {
-    const Consts Kc = consts_from_words(sh.hw);   // wheelbase terms (h set per unit)
-    run_stream_wave<INTEG, PL2>(sh, ctl, total, T, n_cand, n_steps, rc, S, Kc, ecfg.delta_t);
-  } else {
-    run_complete_wave<INTEG, PL2>(sh, ctl, total, T, n_cand, n_steps, rc, rec, S);
-  }
+  if (role >= nres) return;   // registered after the count was taken: no units
+  const Consts Kc = S->h.K;   // wheelbase terms (h set per unit)
+  run_stream_wave<INTEG, PL2>(sh, ctl, total, T, static_cast<int64_t>(role) - 1,
+                              static_cast<int64_t>(nres) - 1, n_cand, n_steps, rc, rec, S, Kc,
+                              ecfg.delta_t);
 }
 
 // Resident blocks of one run instantiation (occupancy x CUs), per device.
@@ -659,6 +824,9 @@ int64_t run_grid(int64_t total_units) {
             hipSuccess ||
         per_cu < 1)
       per_cu = 1;
+#ifdef MPC_RUN_PER_CU
+    per_cu = MPC_RUN_PER_CU;   // A/B builds only
+#endif
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         cus < 1)
       cus = 256;

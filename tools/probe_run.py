@@ -18,7 +18,7 @@ NAMES = {0: "units completed", 1: "unit waits for head (completer)",
          2: "completer ticks waiting for quarters", 3: "completer ticks waiting for head",
          4: "stream ticks waiting for the slot", 5: "stream slot waits",
          8: "selector ticks sweep", 9: "selector ticks emit", 10: "selector ticks advance+pub",
-         11: "sweep polls"}
+         11: "sweep polls", 31: "grid blocks (summed over launches)"}
 
 
 def main():
