@@ -4,45 +4,46 @@
 // Why: a step launched as its own kernel(s) pays, every step, the launch's
 // fill and drain (first control loads in flight with nothing to compute, the
 // last tiles finishing on a part-idle chip) and the one-block selection
-// during which HBM idles: ~6-10 us of a ~37-us config-C step.  In kRotCum
-// mode a candidate's rollout needs no start pose (mpc_device.h step_start /
-// cum_pose), so step j+1's candidates can stream while step j is still being
-// selected; only the final pose transform and the criterion wait for the
-// pose.  One launch streams the K steps' tiles back to back:
+// during which HBM idles.  In kRotCum mode a candidate's rollout needs no
+// start pose (mpc_device.h step_start / cum_pose), so step j+1's candidates
+// can stream while step j is still being selected; only the final pose
+// transform and the criterion wait for the pose.  One launch streams the K
+// steps' tiles back to back:
 //
 //   unit u = (step j, tile) = (u / T, u % T), T = tiles of 512 candidates per
-//   step.  The first block to start selects (run_select_step, one step after
-//   the other); every other block streams the units its completer wave claims
-//   (one counter, increasing unit order, two units ahead: every claimed unit
-//   belongs to a running block, so the lowest unselected unit can always go
-//   on — no residency assumption), with 5 waves:
-//   - waves 0-3 stream (run_stream_wave): one LDS-DMA control ring per wave
-//     that runs ACROSS units (a unit's last steps already issue the next
-//     unit's first rows), the step size h speculated from the last head the
-//     block knows (+ dt per step, as episode_prepare forms it); at a unit's
-//     end a wave parks its lanes' position sums in LDS and goes on — no
-//     barrier, no global load, no wait other than its own control rows;
-//   - wave 4 completes (run_complete_wave): it waits for step j's published
-//     head, turns the parked sums into poses and criteria (recomputing a
-//     quarter whose h was mis-speculated — an episode restart reset t — and
-//     irregular candidates), reduces the unit to one tagged record and frees
-//     the parking slot;
-//   - the selector sweeps step j's T records, re-rolls the winner (emit_winner),
-//     applies the episode update (episode_advance: finishing logic, operator
-//     events, restart, log record, the next step's t and constants) and
-//     publishes step j+1's head.
+//   step.  Blocks register in start order; the first one selects
+//   (run_select_step, one step after the other), the others stream units
+//   s, s + G, s + 2G, ... (streaming block s of G registered ones: every
+//   block that owns units is running, whatever residency the occupancy API
+//   promised).  A streaming block's 4 waves are independent (run_stream_wave):
+//   - each wave streams its quarter (128 candidates) of the block's units with
+//     an LDS-DMA control ring that runs ACROSS units (a unit's last steps
+//     already issue the next unit's first rows), the step size h speculated
+//     from the last head the wave knows (+ dt per step, as episode_prepare
+//     forms it);
+//   - at a unit's end it keeps the quarter's position sums in registers (up
+//     to kRunPend quarters) and goes on; it polls the oldest one's head with
+//     an LDS-DMA that lands behind its counted waits, then scores the quarter
+//     (the final pose transform and criterion; a mis-speculated h — an
+//     episode restart reset t — or an irregular candidate is re-rolled at the
+//     unit's end) and counts it in LDS; the wave whose count completes the
+//     unit writes its tagged record;
+//   - the selector sweeps step j's T records, re-rolls the winner
+//     (emit_winner), applies the episode update (episode_advance: finishing
+//     logic, operator events, restart, log record, the next step's t and
+//     constants) and publishes step j+1's head.
 //
 // Hand-offs (MI355X_MICROARCH.md "inter-workgroup visibility",
 // cdna_hip_programming.md Guideline 16 R2): every handed-off word is an 8-byte
 // {data32 << 32 | tag32} granule written by ONE relaxed agent-scope atomic
-// store (sc1) and read by relaxed agent-scope atomic loads (sc1); the tag is
-// the step index within the call + 1, so a granule validates itself and no
-// fence is needed.  The polled words (abort word, head and record granules)
-// are zeroed by a memset node before every launch (mpc_episode_run), so a tag
-// from an earlier call (or graph replay) never matches.  Inside a block the
-// streaming waves and the completer meet only in LDS.  Every wait is bounded:
-// on a timeout the waiter sets the abort word (every other wait then gives
-// up at once) and chain error 3.
+// store (sc1) and read by relaxed agent-scope loads (sc1); the tag is the
+// step index within the call + 1, so a granule validates itself and no fence
+// is needed.  The polled words (registration, abort word, head and record
+// granules) are zeroed by a memset node before every launch
+// (mpc_episode_run), so a tag from an earlier call (or graph replay) never
+// matches.  Inside a block the waves meet only in LDS.  Every wait is bounded:
+// on a timeout the waiter sets the abort word (every other wait then gives up
+// at once) and chain error 3.
 #pragma once
 
 #include "mpc_episode.h"
@@ -60,10 +61,9 @@ __device__ unsigned long long g_run_stats[32];
 #define RUN_STAT(i, v) atomicAdd(&g_run_stats[i], static_cast<unsigned long long>(v))
 #define RUN_TICK() __builtin_amdgcn_s_memrealtime()
 #define RUN_ACC(i, v) (st_acc[i] += static_cast<uint64_t>(v))
-// per-unit timestamps (units < 1 << 20): 0 stream start, 1 stream end, 2
-// parked, 3 completed, 4 ticks the streaming wave 0 waited for this unit's
-// claim, 5 completer: quarters parked and head known (completion start),
-// 6 claim issued (plain stores by lane 0 of wave 0 / the completer)
+// per-unit timestamps (units < 1 << 20), by lane 0 of wave 0 of the
+// streaming block: 0 stream start, 1 stream end, 2 kept (after a full-hand
+// wait), 3 record written (by the completing wave), 7 the block (plain stores)
 __device__ unsigned long long g_run_ut[1 << 20][8];
 #define RUN_UT(u, f) \
   do { if ((u) < (1 << 20)) g_run_ut[(u)][(f)] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -89,14 +89,25 @@ __device__ unsigned long long g_run_tl[512][5];
 constexpr int kRunRecWords = 4;       // granules per unit record: key hi, key lo, index, pad
 constexpr uint32_t kRunSpinLimit = 1u << 18;   // x s_sleep(16) ~1 us: ~0.25 s
 
+// The published head, in kRunPubCopies copies 4 KiB apart (block b polls copy
+// b % kRunPubCopies) for A/B: 1, 16 and 64 copies ran at the same speed (the
+// ~3000 polling waves do not make the head's lines a hot spot that matters).
+#ifndef MPC_RUN_PUB_COPIES
+#define MPC_RUN_PUB_COPIES 1
+#endif
+constexpr int kRunPubCopies = MPC_RUN_PUB_COPIES;
+struct RunPubCopy {
+  uint64_t pub[2][kHeadDwords];   // head of step j in pub[j & 1], tag j + 1
+  uint8_t pad_[4096 - 2 * kHeadDwords * 8];
+};
 // The polled block at the start of the run workspace (zeroed every call).
 struct RunCtl {
   uint32_t abort;        // a bounded wait timed out: every wait gives up
-  uint32_t claim;        // next unit to hand out (claimed by the completer waves)
+  uint32_t unused_;
   uint32_t role;         // blocks registered (in start order): the first one selects
   uint32_t nres;         // registered blocks when the selector closed the registration
-  uint32_t pad_[28];
-  uint64_t pub[2][kHeadDwords];   // head of step j in pub[j & 1], tag j + 1
+  uint32_t pad_[1020];
+  RunPubCopy copy[kRunPubCopies];
 };
 static_assert(sizeof(RunCtl) % 16 == 0, "memset block: multiple of 16 B");
 
@@ -299,7 +310,10 @@ __device__ __noinline__ void run_select_step(
   }
   __syncthreads();
   // step j+1's head: the streaming blocks' final constants
-  if (!last && q < kHeadDwords) granule_store(rc->pub[(j + 1) & 1] + q, tag + 1u, s_head[q]);
+  if (!last)
+    for (int i = q; i < kRunPubCopies * kHeadDwords; i += kBlock)
+      granule_store(rc->copy[i / kHeadDwords].pub[(j + 1) & 1] + i % kHeadDwords, tag + 1u,
+                    s_head[i % kHeadDwords]);
   if (clock && q == 0) clock[j] = __builtin_amdgcn_s_memrealtime();
   if (q == 0) RUN_TL_MAX(j, 4);
   if (q == 0) {
@@ -316,28 +330,26 @@ __device__ __noinline__ void run_select_step(
   __syncthreads();   // s_log / s_slot reuse
 }
 
-// Per streaming block: the parking slots (one unit each: 4 waves x 64 lanes x
-// two candidates' position sums and irregular flags, the h each wave's loop
-// used) and the quarter minima.  LDS only; the four streaming waves order
-// their accesses with lgkmcnt waits (LDS operations of a wave complete in
-// order) and relaxed LDS atomics.
+// Per streaming block: the quarter minima of its units (unit k in slot
+// k % kRunSlots) and each wave's head-poll buffer.  LDS only; the four
+// streaming waves order their accesses with lgkmcnt waits (LDS operations of
+// a wave complete in order) and relaxed LDS atomics.  A wave keeps its own
+// unscored quarters (position sums) in registers: no parking in LDS, which
+// left room for 4 blocks a CU.
 #ifndef MPC_RUN_SLOTS
-#define MPC_RUN_SLOTS 2
+#define MPC_RUN_SLOTS 4
 #endif
-constexpr int kRunSlots = MPC_RUN_SLOTS;   // parking slots per block (unit k in slot k % kRunSlots)
+constexpr int kRunSlots = MPC_RUN_SLOTS;   // minima slots per block (unit k in slot k % kRunSlots)
 static_assert(kRunSlots >= 1 && kRunSlots <= 8, "MPC_RUN_SLOTS must be in [1, 8]");
 // The run's own control ring (kRunRing - 1 steps in flight per wave).  (4
 // slots: 54272 B of LDS a block, and only 2 blocks per CU became resident.)
 #ifndef MPC_RUN_RING
-#define MPC_RUN_RING 3
+#define MPC_RUN_RING 4
 #endif
 constexpr int kRunRing = MPC_RUN_RING;
 static_assert(kRunRing >= 2 && kRunRing <= 4, "MPC_RUN_RING must be in [2, 4]");
 __shared__ double2 g_run_ring[kWaves][kRunRing][2][64];  // [wave][slot][v|beta][lane]
 struct RunLds {
-  double2 px[kRunSlots][kBlock], py[kRunSlots][kBlock];   // per streaming lane: (A0,A1), (B0,B1)
-  uint64_t badm[kRunSlots][kWaves][2];   // ballot of candidate c irregular, per wave
-  double ph[kRunSlots][kWaves];     // h of each wave's loop
   uint64_t qkey[kRunSlots][kWaves]; // each wave's quarter minimum
   int64_t qidx[kRunSlots][kWaves];
   int32_t cnt[kRunSlots];           // quarters of the slot's unit scored
@@ -427,17 +439,33 @@ __device__ __noinline__ uint64_t run_rescore(const uint64_t* head, double hq, co
   return cost_key(cst);
 }
 
+// A wave's unscored quarter: its lanes' position sums and irregular flags,
+// the h its loop used, the block's unit index and the step.
+struct RunPend {
+  double2 a, b;   // (A0, A1), (B0, B1)
+  uint32_t bad;   // bit c: candidate c irregular
+  double h;
+  int32_t k;
+  int64_t j;
+};
+#ifndef MPC_RUN_PEND
+#define MPC_RUN_PEND 2
+#endif
+constexpr int kRunPend = MPC_RUN_PEND;   // unscored quarters a wave holds (registers)
+static_assert(kRunPend >= 1 && kRunPend <= 4, "MPC_RUN_PEND must be in [1, 4]");
+
 // Streaming wave (waves 0-3 of a streaming block): rolls out its quarter (128
 // candidates: lane l of wave w holds candidates tile*512 + (64w + l)*2 + {0,1})
 // of each of the block's units (s, s + G, s + 2G, ... for streaming block s of
-// G), parks the sums and goes on.  The control ring (kRing slots of one step's
+// G), keeps the sums in registers and goes on.  The control ring (kRing slots of one step's
 // v and beta rows, kRing-1 steps in flight) continues across units.  The
 // wave learns a parked quarter's head by polling it with an LDS-DMA into its
 // own buffer (it lands behind the counted waits two steps later), scores the
 // quarter and counts it; the wave whose count completes the unit combines the
 // four minima into the unit's record and frees the slot.  The only blocking
-// waits: its own control rows, and at a unit's end, when all kRunSlots slots
-// hold this wave's unscored quarters, the oldest one's head.
+// waits: its own control rows; at a unit's end, when the wave already holds
+// kRunPend unscored quarters, the oldest one's head; and a minima slot still
+// holding the unit kRunSlots before (another wave that far behind).
 template <int INTEG, bool PL2>
 __device__ __forceinline__ void run_stream_wave(RunLds& sh, const double* const* __restrict__ ctl,
                                                 int64_t total, int64_t T, int64_t s, int64_t G,
@@ -504,13 +532,11 @@ __device__ __forceinline__ void run_stream_wave(RunLds& sh, const double* const*
 #ifdef MPC_RUN_STATS
   uint64_t st_acc[16] = {0};
 #endif
-  // This wave's parked, unscored quarters: units pk0 .. pk0 + pend_n - 1 of
-  // the block (consecutive; sums in slot k % kRunSlots, speculated h in
-  // sh.ph[slot][wv]).
+  // This wave's unscored quarters, oldest first (e0, then e1).
   const uint32_t pollw = __builtin_amdgcn_readfirstlane(lds_addr(&sh.poll[wv][0]));
+  const RunPubCopy& pubc = rc->copy[s % kRunPubCopies];
   int pend_n = 0;
-  int32_t pk0 = 0;                       // oldest pending unit of the block
-  int64_t pj0 = 0;                       // its step
+  RunPend e0{}, e1{}, e2{}, e3{};   // (entries past kRunPend are never used)
   int64_t khj = 0;                       // latest step whose head this wave took (poll buffer)
   double kt = S->h.t;                    // that head's t (the speculation's base)
   int poll_age = 0;                      // 0: none in flight; else steps waited since issue
@@ -528,19 +554,24 @@ __device__ __forceinline__ void run_stream_wave(RunLds& sh, const double* const*
         static_cast<uint32_t>(sh.poll[wv][kRunTDword + 1] >> 32)));
     return __longlong_as_double(static_cast<long long>((hi << 32) | lo));
   };
-  // score the oldest pending quarter with the head in the poll buffer (step pj0)
-  auto resolve_oldest = [&]() {
-    const int sl = pk0 % kRunSlots;
-    const int64_t u0 = unit_of(pk0);
-    const double ph0 = sh.ph[sl][wv];
+  // score the oldest pending quarter with the head in the poll buffer (step
+  // e0.j).  Inside the streaming loop (slow = false) only the regular case:
+  // the rescoring call there cost the loop its registers (5x slower steps);
+  // it returns false and the quarter waits for the unit's end.
+  auto resolve_oldest = [&](bool slow) -> bool {
+    const int sl = e0.k % kRunSlots;
+    const int64_t u0 = unit_of(e0.k);
+    const int64_t pj0 = e0.j;
+    const double ph0 = e0.h;
     const double tj = head_t();
     const bool hok = ((tj + delta_t) - tj) == ph0;
-    const uint32_t bb = static_cast<uint32_t>((sh.badm[sl][wv][0] >> lane) & 1u) |
-                        (static_cast<uint32_t>((sh.badm[sl][wv][1] >> lane) & 1u) << 1);
-    const double2 px = sh.px[sl][threadIdx.x], py = sh.py[sl][threadIdx.x];
+    const uint32_t bb = e0.bad;
+    const double2 px = e0.a, py = e0.b;
     const int64_t c0 = (u0 - pj0 * T) * (kBlock * CPL) + threadIdx.x * CPL;
     uint64_t k0, k1;
-    if (hok && __ballot(bb != 0u) == 0) {
+    const bool regular = hok && __ballot(bb != 0u) == 0;
+    if (!slow && !regular) return false;
+    if (regular) {
       const Consts K = consts_from_granules(sh.poll[wv]);
       double xx, yy;
       cum_pose(K, px.x, py.x, xx, yy);
@@ -568,6 +599,16 @@ __device__ __forceinline__ void run_stream_wave(RunLds& sh, const double* const*
       di = c0 + 1;
     }
     wave_argmin(dk, di);
+    // the slot still holds unit k - kRunSlots if another wave is that far behind
+    for (uint32_t it = 0; lds_load(&sh.seq[sl]) != e0.k; ++it) {
+      RUN_ACC(4, 1);
+      if ((it & 1023) == 1023 && run_aborted(rc)) break;
+      if (it >= kRunSpinLimit * 8u) {
+        if (lane == 0) run_fail(rc, S, 4);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
     if (lane == 0) {
       sh.qkey[sl][wv] = dk;
       sh.qidx[sl][wv] = di;
@@ -579,10 +620,13 @@ __device__ __forceinline__ void run_stream_wave(RunLds& sh, const double* const*
     prev = __builtin_amdgcn_readfirstlane(prev);
     if (prev == kWaves - 1) {
       lds_order();
-      run_combine(sh, rec, T, sl, pk0, u0, pj0);
+      run_combine(sh, rec, T, sl, e0.k, u0, pj0);
     }
-    ++pk0;
-    if (--pend_n > 0) pj0 = unit_of(pk0) / T;
+    --pend_n;
+    e0 = e1;   // shift (static registers; entries past pend_n are don't-care)
+    if constexpr (kRunPend > 2) e1 = e2;
+    if constexpr (kRunPend > 3) e2 = e3;
+    return true;
   };
   // after a poll has landed: take it if every loop word carries the tag
   auto take_poll = [&]() {
@@ -595,12 +639,13 @@ __device__ __forceinline__ void run_stream_wave(RunLds& sh, const double* const*
       kt = head_t();
     }
     poll_age = 0;
-    while (pend_n > 0 && khj == pj0) resolve_oldest();
+    while (pend_n > 0 && khj == e0.j && resolve_oldest(false)) {
+    }
   };
   // blocking: the head of the oldest pending quarter (relaxed polls)
   auto wait_oldest = [&]() {
-    const uint64_t* g = rc->pub[pj0 & 1];
-    const uint32_t tag = static_cast<uint32_t>(pj0 + 1);
+    const uint64_t* g = pubc.pub[e0.j & 1];
+    const uint32_t tag = static_cast<uint32_t>(e0.j + 1);
     const uint64_t w0 = RUN_TICK();
     for (uint32_t it = 0;; ++it) {
       const uint64_t w = run_loop_word(lane) ? granule_load(g + lane) : 0ull;
@@ -616,12 +661,12 @@ __device__ __forceinline__ void run_stream_wave(RunLds& sh, const double* const*
       __builtin_amdgcn_s_sleep(4);
     }
     lds_order();
-    khj = pj0;
+    khj = e0.j;
     kt = head_t();
     poll_age = 0;
     RUN_ACC(5, 1);
     RUN_ACC(6, RUN_TICK() - w0);
-    while (pend_n > 0 && khj == pj0) resolve_oldest();
+    while (pend_n > 0 && khj == e0.j) resolve_oldest(true);
   };
   for (int32_t k = 0; u < total; ++k, u = unit_of(k)) {
     const int64_t j = u / T;
@@ -668,49 +713,40 @@ __device__ __forceinline__ void run_stream_wave(RunLds& sh, const double* const*
       // counted waits later (R-1 more row pairs issued behind it), then taken
       if (poll_age > 0 && ++poll_age >= R) take_poll();
       if (pend_n > 0 && poll_age == 0) {
-        poll_j = pj0;
+        poll_j = e0.j;
         lds_order();   // this wave's reads of the previous poll are done
-        if (lane < 32) glds_poll(rc->pub[pj0 & 1] + 2 * lane, pollw);
+        if (lane < 32) glds_poll(pubc.pub[e0.j & 1] + 2 * lane, pollw);
         poll_age = 1;
       }
     }
     if (lane == 0 && wv == 0) RUN_UT(u, 1);
-    // the slot of unit k held unit k - kRunSlots: if that one is still this
-    // wave's to score, wait for its head; then wait until the unit is combined
-    const int sl = k % kRunSlots;
-    if (pend_n == kRunSlots) {
+    // a full hand: the oldest quarter's head first
+    if (pend_n == kRunPend) {
       if (poll_age > 0) wait_vm<0>();    // (an in-flight poll must land first)
       poll_age = 0;
       wait_oldest();
     }
-    const uint64_t p0t = RUN_TICK();
-    for (uint32_t it = 0; lds_load(&sh.seq[sl]) != k; ++it) {
-      if ((it & 1023) == 1023 && run_aborted(rc)) break;
-      if (it >= kRunSpinLimit * 8u) {
-        if (lane == 0) run_fail(rc, S, 4);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    RUN_ACC(4, RUN_TICK() - p0t);
     if (lane == 0 && wv == 0) RUN_UT(u, 2);
-    sh.px[sl][threadIdx.x] = make_double2(x[0], x[1]);
-    sh.py[sl][threadIdx.x] = make_double2(y[0], y[1]);
     {
-      const uint64_t b0 = __ballot(bad[0]), b1 = __ballot(bad[1]);
-      if (lane == 0) {
-        sh.badm[sl][wv][0] = b0;
-        sh.badm[sl][wv][1] = b1;
-        sh.ph[sl][wv] = Kl.h;
-      }
+      RunPend e;
+      e.a = make_double2(x[0], x[1]);
+      e.b = make_double2(y[0], y[1]);
+      e.bad = (bad[0] ? 1u : 0u) | (bad[1] ? 2u : 0u);
+      e.h = Kl.h;
+      e.k = k;
+      e.j = j;
+      if (pend_n == 0)
+        e0 = e;
+      else if (kRunPend == 2 || pend_n == 1)
+        e1 = e;
+      else if (kRunPend == 3 || pend_n == 2)
+        e2 = e;
+      else
+        e3 = e;
+      ++pend_n;
     }
-    if (pend_n++ == 0) {
-      pk0 = k;
-      pj0 = j;
-    }
-    lds_order();
     // this wave already holds the head of its oldest pending step: score now
-    while (pend_n > 0 && khj == pj0) resolve_oldest();
+    while (pend_n > 0 && khj == e0.j) resolve_oldest(true);
   }
   if (poll_age > 0) wait_vm<0>();
   while (pend_n > 0) wait_oldest();   // the wave's last quarters
@@ -722,13 +758,13 @@ __device__ __forceinline__ void run_stream_wave(RunLds& sh, const double* const*
 }
 
 constexpr int kRunThreads = kBlock;   // 4 waves: the selector's, or a streaming block's
-// Launch bound: waves per SIMD.  LDS (~46 KB a block) allows 3 blocks of 4
-// waves per CU; asking for more than LDS allows makes the bound void for the
-// out-of-line callees (run_rescore then took 180 VGPRs: 2 blocks per CU).
+// Launch bound: waves per SIMD (4 blocks of 4 waves per CU).  It must not ask
+// for more than LDS allows: that makes the bound void for the out-of-line
+// callees (run_rescore then took 180 VGPRs, 2 blocks per CU).
 #ifndef MPC_RUN_WAVES
 #define MPC_RUN_WAVES 3
 #endif
-constexpr uint32_t kRunRegisterTicks = 2000;   // s_memrealtime (100 MHz): 20 us
+constexpr uint32_t kRunRegisterTicks = 1000;   // s_memrealtime (100 MHz): 10 us without a new block
 
 // ctl: device array [k_steps][2] of the steps' control SoA pointers (v, beta).
 // rec: [2][T][kRunRecWords] record granules (step j in half j & 1).
@@ -736,8 +772,8 @@ constexpr uint32_t kRunRegisterTicks = 2000;   // s_memrealtime (100 MHz): 20 us
 // clock: optional [k_steps] s_memrealtime (100 MHz) when step j was completed.
 //
 // Roles: blocks register in start order (rc->role).  The first one selects;
-// it closes the registration when every block of the grid is in, or 20 us
-// after it started with at least one other block in, and publishes the count
+// it closes the registration when every block of the grid is in, or when no
+// block has come in for 10 us (at least one other in), and publishes the count
 // N (rc->nres).  Blocks 1 .. N-1 stream units s, s + G, ... (s = role - 1,
 // G = N - 1): every block with a unit is running, whatever the residency the
 // occupancy API promised.  A block that registers later has no unit.
@@ -759,10 +795,17 @@ __global__ __launch_bounds__(kRunThreads, MPC_RUN_WAVES) void k_episode_run(
     uint32_t n = 0;
     if (r == 0) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint64_t tc = t0;   // when the count last grew
+      uint32_t last = 0;
       for (;;) {
         n = __hip_atomic_load(&rc->role, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t dt = __builtin_amdgcn_s_memrealtime() - t0;
-        if (n >= gridDim.x || (n >= 2 && dt > kRunRegisterTicks) || dt > 1000 * kRunRegisterTicks)
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (n != last) {
+          last = n;
+          tc = now;
+        }
+        if (n >= gridDim.x || (n >= 2 && now - tc > kRunRegisterTicks) ||
+            now - t0 > 1000 * kRunRegisterTicks)
           break;
         __builtin_amdgcn_s_sleep(8);
       }

@@ -14,11 +14,10 @@ from diplomjourney_amd import math_model_tree as mmt, native  # noqa: E402
 from diplomjourney_amd.episode import DeviceEpisode  # noqa: E402
 from diplomjourney_amd.expansion import Expansion  # noqa: E402
 
-NAMES = {0: "units completed", 1: "unit waits for head (completer)",
-         2: "completer ticks waiting for quarters", 3: "completer ticks waiting for head",
-         4: "stream ticks waiting for the slot", 5: "stream slot waits",
+NAMES = {1: "quarters re-rolled at a unit's end", 4: "minima-slot spins",
+         5: "full-hand waits (wave x unit)", 6: "full-hand wait ticks (sum over waves)",
          8: "selector ticks sweep", 9: "selector ticks emit", 10: "selector ticks advance+pub",
-         11: "sweep polls", 31: "grid blocks (summed over launches)"}
+         11: "sweep polls", 31: "registered blocks (summed over launches)"}
 
 
 def main():
@@ -55,11 +54,11 @@ def main():
     per = [(b - a) * 10e-3 for a, b in zip(c, c[1:])]
     per.sort()
     print(f"n={n} ns={ns} K={K}: {dt / K * 1e6:.1f} us/step wall, period p50 {per[len(per) // 2]:.1f} us")
-    u = max(1, st[0])
+    u = max(1, st[5])
     for i, name in NAMES.items():
         extra = ""
         if "ticks" in name and "selector" not in name:
-            extra = f"  -> {st[i] / u * 10e-3:.2f} us per unit (sum over waves)"
+            extra = f"  -> {st[i] / u * 10e-3:.2f} us per wait"
         if "selector" in name:
             extra = f"  -> {st[i] / K * 10e-3:.2f} us per step"
         print(f"  {name:32s} {st[i]}{extra}")

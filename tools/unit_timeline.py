@@ -1,5 +1,5 @@
 """Per-unit timeline of the persistent run (debug variant -DMPC_RUN_STATS):
-per step, when its units started / ended streaming, were parked and
+per step, when its units started / ended streaming, were kept and
 completed, against the selection (published head) times.
     DIPLOMJOURNEY_MPC_LIB=tools/var_stats.so python tools/unit_timeline.py [n] [ns] [K]"""
 import ctypes
@@ -39,8 +39,7 @@ def main():
     buf = np.zeros(nu * 8, dtype=np.uint64)
     ut(buf.ctypes.data, nu)
     raw = buf.reshape(nu, 8).astype(np.float64)
-    claimw = raw[:, 4] * 1e-2
-    t = raw[:, [0, 1, 2, 3, 5, 6]]
+    t = raw[:, [0, 1, 2, 3]]   # stream start, stream end, kept, record written
     pub = clock.cpu().numpy().astype(np.float64)   # step j's successor head published
     t0 = t[:T, 0].min()
     t = (t - t0) * 1e-2
@@ -48,7 +47,7 @@ def main():
     steps = min(K, nu // T)
     print(f"n={n} ns={ns} K={K} T={T}; us from the first unit start")
     print("step: start[min,med,max]  end[min,med,max]  complete[max]  P_j(head j published)  "
-          "parked-wait med  end-start med")
+          "kept->record med  end-start med")
     for j in list(range(0, 4)) + list(range(steps // 2, steps // 2 + 6)):
         u = t[j * T:(j + 1) * T]
         pj = pub[j - 1] if j > 0 else 0.0
@@ -58,21 +57,17 @@ def main():
     mid = slice((steps // 4) * T, (3 * steps // 4) * T)
     m = t[mid]
     print("medians over the middle half: stream (end-start)", np.median(m[:, 1] - m[:, 0]),
-          "| slot wait (parked-end)", np.median(m[:, 2] - m[:, 1]),
-          "| park->complete", np.median(m[:, 3] - m[:, 2]))
+          "| full-hand wait (kept-end)", np.median(m[:, 2] - m[:, 1]),
+          "| kept->record", np.median(m[:, 3] - m[:, 2]))
     per = np.diff(pub[steps // 4: 3 * steps // 4])
     print("period median", np.median(per), "chain_error", ep.chain_error())
-    print("medians: claim wait at the crossing", np.median(claimw[mid]),
-          "| claim issued -> stream start", np.median(m[:, 0] - m[:, 5]),
-          "| parked -> completion start", np.median(m[:, 4] - m[:, 2]),
-          "| completion start -> done", np.median(m[:, 3] - m[:, 4]))
-    # units whose head was out when they parked
+    # units whose head was out when they were kept
     jj = np.arange(nu)[mid] // T
     pj = np.array([pub[j - 1] if j > 0 else -1e9 for j in jj])
     known = m[:, 2] >= pj
-    print("units parked with their head already out:", known.mean(),
-          "| their parked -> completion start", np.median((m[:, 4] - m[:, 2])[known]),
-          "| others: head out -> completion start", np.median((m[:, 4] - pj)[~known]))
+    print("units kept with their head already out:", known.mean(),
+          "| their kept -> record", np.median((m[:, 3] - m[:, 2])[known]),
+          "| others: head out -> record", np.median((m[:, 3] - pj)[~known]))
     # per block: busy (streaming) vs the gaps between its units
     blk = buf.reshape(nu, 8)[:, 7].astype(np.int64)[mid]
     lo, hi = m[:, 0].min(), m[:, 1].max()
@@ -86,7 +81,20 @@ def main():
         gaps_next += list(r[1:, 0] - r[:-1, 2])
     span = hi - lo
     print(f"blocks seen {nblk}; streaming fraction {busy / (nblk * span):.2f} of {span:.0f} us")
-    for name, g in (("end->parked", gaps_park), ("parked->next start", gaps_next)):
+    st = m[:, 1] - m[:, 0]
+    print("stream time per unit: p10 %.2f p50 %.2f p90 %.2f p99 %.2f max %.2f" %
+          tuple(np.percentile(st, [10, 50, 90, 99, 100])))
+    per_blk = np.array([st[blk == b].mean() for b in np.unique(blk)])
+    print("per-block mean stream time: p10 %.2f p50 %.2f p90 %.2f max %.2f" %
+          tuple(np.percentile(per_blk, [10, 50, 90, 100])))
+    # lag: how far each block's unit starts trail the step's first start
+    jj_mid = np.arange(nu)[mid] // T
+    first = {j: m[jj_mid == j, 0].min() for j in np.unique(jj_mid)}
+    lag = m[:, 0] - np.array([first[j] for j in jj_mid])
+    lag_blk = np.array([lag[blk == b].mean() for b in np.unique(blk)])
+    print("per-block mean start lag behind the step's first start: p10 %.1f p50 %.1f p90 %.1f max %.1f"
+          % tuple(np.percentile(lag_blk, [10, 50, 90, 100])))
+    for name, g in (("end->kept", gaps_park), ("kept->next start", gaps_next)):
         g = np.array(g)
         print(f"  {name}: p50 {np.percentile(g, 50):.2f} p90 {np.percentile(g, 90):.2f} "
               f"p99 {np.percentile(g, 99):.2f} mean {g.mean():.2f} us")
