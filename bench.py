@@ -120,7 +120,7 @@ def parse():
                     help="override the workload's per-GPU candidate count")
     ap.add_argument("--dump-log", default=None,
                     help="write the device episode's per-step log (rank 0) to this JSON file")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r01_traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r02_traffic.json"),
                     help="PMC-derived HBM bytes per launch for the roofline 'traffic' field "
                          "(tools/pmc.sh + tools/pmc_summary.py on the same kernel and config)")
     args = ap.parse_args()
