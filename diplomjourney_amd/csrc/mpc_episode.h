@@ -430,7 +430,10 @@ __device__ __forceinline__ bool chain_read(const EpisodeState* S, uint32_t epoch
 }
 
 #ifndef MPC_CHAIN_WAVES
-#define MPC_CHAIN_WAVES 4   // launch bound of the chained kernel (5 spills: block 0's finalize)
+#define MPC_CHAIN_WAVES 5   // launch bound of the chained kernel: waves per SIMD
+#endif
+#ifndef MPC_CHAIN_PIN
+#define MPC_CHAIN_PIN false
 #endif
 // PL2 (wheelbase a power of two) is a template parameter, not a runtime
 // branch: with both rollout variants inlined the kernel held 119 VGPRs and
@@ -545,7 +548,10 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
     // ignored), so every lane reaches the barriers of pre0 / wait on the same path
     const int64_t cl = c0 < n_cand ? c0 : n_cand - CPL;
     double cst[CPL];
-    rollout_lane_glds_k<INTEG, ROT, PL2>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0, mid);
+    // leading trig coefficients not pinned: the fifth wave per SIMD needs the
+    // registers more (as the rect+cum stream kernel)
+    rollout_lane_glds_k<INTEG, ROT, PL2, decltype(wait), decltype(pre0), decltype(mid),
+                        MPC_CHAIN_PIN>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0, mid);
     Kl = K;            // later tiles: the final constants
     if (c0 < n_cand) {
 #pragma unroll

@@ -310,86 +310,95 @@ __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Const
   const uint32_t ring0 = __builtin_amdgcn_readfirstlane(lds_addr(&g_ring[wv][0][0][0]));
   constexpr uint32_t kSlot = 2 * 64 * sizeof(double2);  // 2 KiB
   auto dst = [&](int slot) { return ring0 + slot * kSlot; };
-#pragma unroll
-  for (int u = 0; u < R - 1; ++u)
-    if (u < n_steps && MPC_EXPERIMENT != 2)
-      glds_pair(v + u * ld + c0, b + u * ld + c0, dst(u), dst(u) + kSlot / 2);
-  if constexpr (ROT != kRotCum)
-    pre();
-  else
-    pre0();   // kRotCum: the loop constants Kloop (the chained step reads them here)
-  double x[CPL], y[CPL], ph[CPL], sn[CPL], cs[CPL];
-  bool bad[CPL];
-#pragma unroll
-  for (int j = 0; j < CPL; ++j) {
-    step_start<ROT>(Kloop, x[j], y[j], ph[j], sn[j], cs[j]);
-    bad[j] = false;
-  }
-  double2 v2 = make_double2(0.0, 0.0), b2 = v2;   // the last slot's contents as read
   // leading trig coefficients pinned in VGPRs (opaque to the compiler, so not
   // re-materialised per step)
   trig::Leads lead = trig::const_leads();
   if constexpr (PIN)
     asm volatile("" : "+v"(lead.tp), "+v"(lead.tq), "+v"(lead.rs), "+v"(lead.rc));
+  // The loop constants: Kloop (read after pre0), or K when a speculated step
+  // size turns out wrong (kRotCum with a real pre(): the chained step after an
+  // episode restart) and the loop runs again from the controls with the final
+  // constants — the same code, bitwise the lane's arithmetic, and no second
+  // copy of the recurrence to hold registers for.
+  Consts KL;
+  double x[CPL], y[CPL], ph[CPL], sn[CPL], cs[CPL];
+  bool bad[CPL];
+  for (int pass = 0;; ++pass) {
+#pragma unroll
+    for (int u = 0; u < R - 1; ++u)
+      if (u < n_steps && MPC_EXPERIMENT != 2)
+        glds_pair(v + u * ld + c0, b + u * ld + c0, dst(u), dst(u) + kSlot / 2);
+    if (pass == 0) {
+      if constexpr (ROT != kRotCum)
+        pre();
+      else
+        pre0();   // kRotCum: the loop constants Kloop (the chained step reads them here)
+      KL = Kloop;
+    }
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      step_start<ROT>(KL, x[j], y[j], ph[j], sn[j], cs[j]);
+      bad[j] = false;
+    }
+    double2 v2 = make_double2(0.0, 0.0), b2 = v2;   // the last slot's contents as read
 #pragma unroll 1
-  for (int s = 0; s < n_steps; s += R) {
+    for (int s = 0; s < n_steps; s += R) {
 #pragma unroll
-    for (int u = 0; u < R; ++u) {
-      const int st = s + u;
-      if (st < n_steps) {
-        if (MPC_EXPERIMENT == 2) {
-        } else if (st + R - 1 < n_steps) {
-          const int sr = st + R - 1, slot = (u + R - 1) % R;   // = the slot read last step
-          glds_refill(v + sr * ld + c0, b + sr * ld + c0, dst(slot), dst(slot) + kSlot / 2, v2,
-                      b2);
-          wait_vm<2 * (R - 1)>();   // this step's pair has landed
-        } else {
-          wait_vm<0>();             // pipeline tail
-        }
-        if constexpr (!std::is_same_v<Mid, NoPre>) {
-          if (st == n_steps - 3) mid();
-        }
-        v2 = g_ring[wv][u][0][lane];
-        b2 = g_ring[wv][u][1][lane];
+      for (int u = 0; u < R; ++u) {
+        const int st = s + u;
+        if (st < n_steps) {
+          if (MPC_EXPERIMENT == 2) {
+          } else if (st + R - 1 < n_steps) {
+            const int sr = st + R - 1, slot = (u + R - 1) % R;   // = the slot read last step
+            glds_refill(v + sr * ld + c0, b + sr * ld + c0, dst(slot), dst(slot) + kSlot / 2, v2,
+                        b2);
+            wait_vm<2 * (R - 1)>();   // this step's pair has landed
+          } else {
+            wait_vm<0>();             // pipeline tail
+          }
+          if constexpr (!std::is_same_v<Mid, NoPre>) {
+            if (st == n_steps - 3) mid();
+          }
+          v2 = g_ring[wv][u][0][lane];
+          b2 = g_ring[wv][u][1][lane];
 #if MPC_EXPERIMENT == 1
-        x[0] += v2.x * b2.x;
-        x[1] += v2.y * b2.y;
-        continue;
+          x[0] += v2.x * b2.x;
+          x[1] += v2.y * b2.y;
+          continue;
 #elif MPC_EXPERIMENT == 2
-        v2 = make_double2(0.5 + 1e-3 * ((c0 + st) & 15), 0.5 + 1e-3 * ((c0 + 1 + st) & 15));
-        b2 = make_double2(0.01 * ((c0 >> 4) & 31) - 0.15, 0.01 * (((c0 + 1) >> 4) & 31) - 0.15);
+          v2 = make_double2(0.5 + 1e-3 * ((c0 + st) & 15), 0.5 + 1e-3 * ((c0 + 1 + st) & 15));
+          b2 = make_double2(0.01 * ((c0 >> 4) & 31) - 0.15, 0.01 * (((c0 + 1) >> 4) & 31) - 0.15);
 #endif
-        // the heading itself is not needed here (rotation mode carries sin/cos;
-        // an irregular candidate is recomputed from K.phi), so no phi chain
-        double ph0 = ROT ? 0.0 : ph[0], ph1 = ROT ? 0.0 : ph[1];
-        step_core<INTEG, ROT, PL2>(x[0], y[0], ph0, sn[0], cs[0], v2.x, b2.x, Kloop, bad[0],
-                                   &lead);
-        step_core<INTEG, ROT, PL2>(x[1], y[1], ph1, sn[1], cs[1], v2.y, b2.y, Kloop, bad[1],
-                                   &lead);
-        if (!ROT) {
-          ph[0] = ph0;
-          ph[1] = ph1;
+          // the heading itself is not needed here (rotation mode carries sin/cos;
+          // an irregular candidate is recomputed from K.phi), so no phi chain
+          double ph0 = ROT ? 0.0 : ph[0], ph1 = ROT ? 0.0 : ph[1];
+          step_core<INTEG, ROT, PL2>(x[0], y[0], ph0, sn[0], cs[0], v2.x, b2.x, KL, bad[0],
+                                     &lead);
+          step_core<INTEG, ROT, PL2>(x[1], y[1], ph1, sn[1], cs[1], v2.y, b2.y, KL, bad[1],
+                                     &lead);
+          if (!ROT) {
+            ph[0] = ph0;
+            ph[1] = ph1;
+          }
         }
       }
     }
-  }
-  if constexpr (ROT == kRotCum) {
-    // the start pose is first needed here (chained step: this step's
-    // constants are waited for now; if the step size speculated for the loop
-    // turns out different — an episode restart reset t — the lane recomputes)
-    pre();
-    if constexpr (!std::is_same_v<Pre, NoPre>) {
-      if (Kloop.h != K.h) {   // rare (episode restart): the per-candidate form,
-        // bitwise the lane's arithmetic (tests/test_replica.py), no second ring loop
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          cst[j] = rollout_candidate_l<INTEG, ROT, PL2>(K, v, b, ld, c0 + j, n_steps, nullptr);
-        return;
+    if constexpr (ROT == kRotCum) {
+      // the start pose is first needed here (chained step: this step's
+      // constants are waited for now; if the step size speculated for the loop
+      // turns out different — an episode restart reset t — the loop runs again)
+      if (pass == 0) pre();
+      if constexpr (!std::is_same_v<Pre, NoPre>) {
+        if (KL.h != K.h) {   // rare (episode restart); uniform over the block
+          KL = K;
+          continue;
+        }
       }
-    }
 #pragma unroll
-    for (int j = 0; j < CPL; ++j)
-      if (!bad[j]) cum_pose(K, x[j], y[j], x[j], y[j]);
+      for (int j = 0; j < CPL; ++j)
+        if (!bad[j]) cum_pose(K, x[j], y[j], x[j], y[j]);
+    }
+    break;
   }
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
