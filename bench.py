@@ -17,8 +17,11 @@ A "step" is one MPC step of the device-resident episode (state in HBM, no
 host synchronisation inside the loop):
   --inputs resident (default)  the step's candidate batch is already in HBM
       (a distinct synthetic batch per step, generated before the timed
-      region): rollout/arg-min kernel -> finalize kernel (winner re-roll +
-      episode update: finishing logic, operator events, next step's problem)
+      region).  Default (--integrator rect+cum): ONE chained launch per step,
+      the rollout/arg-min of step k + the completion of step k-1 (winner
+      re-roll + episode update: finishing logic, operator events, next step's
+      problem).  --no-chain or another integrator: rollout
+      kernel -> finalize kernel
   --inputs sampled  the device sampler first regenerates the candidates on the
       grid around the episode's current control (the reference's per-step
       grid), then the same two kernels
@@ -29,10 +32,11 @@ rehearsals launch eagerly); p50/p90 come from a separate
 eager pass with HIP events; `other_inputs` repeats the run with the other
 input mode.  --host-loop runs the host-driven episode instead.
 
-Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel
-(k_rollout_argmin_stream): algorithmic bytes 16 B per candidate-step (fp64 v and
-beta read once) / its average duration, from HIP events around 100
-back-to-back launches on the episode's stream and controls.
+Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the
+chained k_episode_chain by default, k_rollout_argmin_stream for two-launch
+steps): algorithmic bytes 16 B per candidate-step (fp64 v and beta read once)
+/ its average duration, from HIP events around 100 back-to-back launches on
+the episode's stream and controls.
 `cpu_baseline` is the reference-structured Python port (scipy quad) on this
 host's cores, rank 0 at N=1 only, on a bounded sample of the same candidates;
 it runs before the GPU is initialised (it forks worker processes).
@@ -82,12 +86,14 @@ def parse():
                          "fixed graph-launch + sync cost (~0.2 ms) is amortised; 50 for F/G)")
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="C", choices=sorted(WORKLOADS))
-    ap.add_argument("--integrator", default="rect+rot",
+    ap.add_argument("--integrator", default=None,
                     choices=["rect+cum", "rect+rot", "rect", "qk21+rot", "qk21"],
                     help="kernel arithmetic (DESIGN.md 'Integrators'): qk21 = the reference's "
                          "quad() bit for bit, rect = direct h*f; +rot = heading carried as "
                          "(sin, cos) and rotated per step; +cum = rotated from the identity, "
-                         "start pose applied last (enables chained steps)")
+                         "start pose applied last (enables chained steps, one launch per "
+                         "step). Default: rect+cum for the episode workloads B/C/D, rect+rot "
+                         "for E/F/G")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="per-core time budget of the cpu_baseline sample (0 = skip)")
     ap.add_argument("--host-loop", action="store_true",
@@ -120,10 +126,13 @@ def parse():
                     help="override the workload's per-GPU candidate count")
     ap.add_argument("--dump-log", default=None,
                     help="write the device episode's per-step log (rank 0) to this JSON file")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r02_traffic.json"),
+    ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per launch for the roofline 'traffic' field "
-                         "(tools/pmc.sh + tools/pmc_summary.py on the same kernel and config)")
+                         "(tools/pmc.sh + tools/pmc_summary.py on the same kernel and config; "
+                         "default: the committed round-2 summary of the roofline's kernel)")
     args = ap.parse_args()
+    if args.integrator is None:
+        args.integrator = "rect+cum" if args.workload in ("B", "C", "D") else "rect+rot"
     if args.steps is None:
         args.steps = 50 if args.workload in ("F", "G") else 500
     return args
@@ -223,6 +232,12 @@ def main():
                            chain=not args.no_chain and args.integrator == "rect+cum")
     pool = make_pool(eng, ep, n_steps, args.steps) if inputs == "resident" else None
     persistent = args.run
+    # the launch that carries the step: the chained kernel (rollout of step k +
+    # completion of step k-1), the persistent run, or the rollout kernel
+    chained = (not persistent and not exchange and getattr(ep, "chain", False)
+               and inputs == "resident")
+    kernel = ("k_episode_run" if persistent else
+              "k_episode_chain" if chained else "k_rollout_argmin_stream")
     if persistent and (exchange or args.host_loop or inputs != "resident"
                        or args.integrator != "rect+cum"):
         raise SystemExit("--run: one GPU, resident inputs, --integrator rect+cum")
@@ -234,7 +249,9 @@ def main():
         main_run = run_steps(args, ep, pool, use_graph, world, device)
         use_graph = main_run["graph"]
         kern_ms = main_run["kernel_in_step_ms"]
-        if hasattr(ep, "partials"):
+        if chained:
+            kern_ms = chain_pass(ep, pool)
+        elif hasattr(ep, "partials"):
             kern_ms = kernel_pass(ep, pool if pool is not None else
                                   make_pool(eng, ep, n_steps, 4))
     other = None
@@ -293,8 +310,7 @@ def main():
                      "(selection published) inside the timed persistent launch" if persistent else
                      "GPU time per MPC step (HIP events between step starts, eager launches)"),
         "kernel_ms": kern_ms, "kernel_in_step_ms": main_run["kernel_in_step_ms"],
-        "roofline": roofline(achieved, bytes_launch, args.traffic_json,
-                             kernel="k_episode_run" if persistent else "k_rollout_argmin_stream"),
+        "roofline": roofline(achieved, bytes_launch, args.traffic_json, kernel=kernel),
         "other_inputs": other,
         "cpu_baseline": cpu,
     }
@@ -475,14 +491,39 @@ def kernel_pass(ep, pool, reps=100):
     return k0.elapsed_time(k1) / reps
 
 
+TRAFFIC_JSON = {"k_rollout_argmin_stream": "r02_traffic.json",
+                "k_episode_chain": "r02_traffic_chain.json"}
+
+
+def chain_pass(ep, pool, reps=100):
+    """The chained launch (rollout of step k + completion of step k-1): REPS
+    back-to-back launches between two HIP events on the launch stream,
+    rotating over the resident batches as kernel_pass does; the episode goes
+    on (the launches are real steps)."""
+    import torch
+    k0 = torch.cuda.Event(enable_timing=True)
+    k1 = torch.cuda.Event(enable_timing=True)
+    ep.step(controls=pool[0])
+    k0.record()
+    for i in range(reps):
+        ep.step(controls=pool[(i + 1) % len(pool)])
+    k1.record()
+    ep.flush()
+    torch.cuda.synchronize()
+    return k0.elapsed_time(k1) / reps
+
+
 def roofline(achieved, bytes_launch, traffic_json, kernel="k_rollout_argmin_stream"):
     """traffic: HBM bytes per launch from the committed PMC summary, used only
-    when it was measured on a launch of the same algorithmic size."""
+    when it was measured on the same kernel at the same algorithmic size."""
     traffic, src = None, None
+    if traffic_json is None and kernel in TRAFFIC_JSON:
+        traffic_json = os.path.join(REPO, "profiles", TRAFFIC_JSON[kernel])
     if traffic_json and os.path.exists(traffic_json):
         with open(traffic_json) as fh:
             t = json.load(fh)
-        if abs(t.get("algorithmic_bytes_per_launch", -1) - bytes_launch) < 1:
+        if (abs(t.get("algorithmic_bytes_per_launch", -1) - bytes_launch) < 1
+                and t.get("kernel", kernel) == kernel):
             traffic, src = t.get("hbm_bytes_per_launch"), os.path.relpath(traffic_json, REPO)
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,

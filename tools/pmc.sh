@@ -16,3 +16,4 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES" \
   timeout -k 10 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o p -- python3 tools/prof_kernel.py ${ARGS:-} > $OUT/pmc$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/pmc$i.log; }
 done
 ls -R $OUT | head -50
+# summary: KERNEL=k_episode_chain ARGS="1000000 10 chain 20 4" for the chained step

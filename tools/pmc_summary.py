@@ -1,7 +1,7 @@
 """Summarise tools/pmc.sh counter passes for the rollout kernel into a JSON
 file bench.py reads for roofline.traffic (--traffic-json).
 
-    python tools/pmc_summary.py gpurun_out/<tag> out.json [algorithmic_bytes]
+    python tools/pmc_summary.py gpurun_out/<tag> out.json [algorithmic_bytes] [kernel]
 
 HBM bytes per launch = 2 x FETCH_SIZE (KB x 1024) + WRITE_SIZE: on gfx950
 FETCH_SIZE counts half the bytes of a 16-B-per-lane streaming read and
@@ -17,10 +17,11 @@ import sys
 def main():
     root, out = sys.argv[1], sys.argv[2]
     algo = float(sys.argv[3]) if len(sys.argv) > 3 else 160e6   # 16 B x N x C of the runs
+    kernel = sys.argv[4] if len(sys.argv) > 4 else "k_rollout_argmin_stream"
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     for f in sorted(glob.glob(os.path.join(root, "pmc*", "p_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
-            if "k_rollout_argmin" not in r["Kernel_Name"]:
+            if kernel not in r["Kernel_Name"]:
                 continue
             per[r["Counter_Name"]][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
     med = {}
@@ -30,7 +31,7 @@ def main():
     fetch_b = med.get("FETCH_SIZE", 0.0) * 1024.0
     write_b = med.get("WRITE_SIZE", 0.0) * 1024.0
     res = {
-        "kernel": "k_rollout_argmin_stream",
+        "kernel": kernel,
         "hbm_bytes_per_launch": 2.0 * fetch_b + write_b,
         "algorithmic_bytes_per_launch": algo,
         "fetch_size_bytes_raw": fetch_b, "write_size_bytes": write_b,

@@ -2,7 +2,9 @@
 batches, then launch only the rollout kernel `reps` times rotating over them
 (B x batch bytes between two uses of a batch > 256 MiB Infinity Cache, so the
 launches stream from HBM as in the bench).
-    python tools/prof_kernel.py [n_cand] [n_steps] [integ] [reps] [batches]"""
+    python tools/prof_kernel.py [n_cand] [n_steps] [integ] [reps] [batches]
+integ "chain": chained rect+cum episode steps instead (mpc_episode_chain_step,
+the bench default's launch: rollout of step k + completion of step k-1)."""
 import os
 import sys
 
@@ -26,9 +28,16 @@ def main():
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
     pool = [eng.sample_controls(V, B, n, ns, 7 + i) for i in range(nb)]
-    prob = make_problem(0.0, 0.0, 0.3, 2, 3, 0, 0, 0.5, 0.05, 0.1)
-    for i in range(reps):
-        eng.partials(prob, *pool[i % nb], integ)
+    if integ == "chain":
+        from diplomjourney_amd.episode import DeviceEpisode
+        ep = DeviceEpisode(eng, n, ns, integrator="rect+cum", chain=True, log_capacity=8192)
+        for i in range(reps):
+            ep.step(controls=pool[i % nb])
+        ep.flush()
+    else:
+        prob = make_problem(0.0, 0.0, 0.3, 2, 3, 0, 0, 0.5, 0.05, 0.1)
+        for i in range(reps):
+            eng.partials(prob, *pool[i % nb], integ)
     torch.cuda.synchronize()
     print("done", n, ns, integ, reps, nb)
 
