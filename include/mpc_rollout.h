@@ -267,12 +267,14 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
  * same controls, bit for bit.  Step j streams the caller-resident controls
  * ctl[2j] (v_sc) / ctl[2j+1] (beta_sc): `ctl` is a DEVICE array of 2*k_steps
  * pointers, each 16-B aligned, [n_steps][n_cand] fp64, n_cand even.  Units of
- * 512 candidates are claimed in order by the launch's blocks; step j+1's
- * candidates stream while step j is being selected (the kRotCum rollout needs
- * the start pose only for its final transform), and the block that claimed
- * step j's last unit reduces its records, re-rolls the winner and applies the
- * episode update (finishing logic, operator events, restart, log record, next
- * step's constants), publishing step j+1's head in tagged words.
+ * 512 candidates (step, tile) go round-robin to the launch's registered
+ * streaming blocks; step j+1's candidates stream while step j is being
+ * selected (the kRotCum rollout needs the start pose only for its final
+ * transform), and one selecting block reduces step j's unit records, re-rolls
+ * the winner and applies the episode update (finishing logic, operator
+ * events, restart, log record, next step's constants), publishing step j+1's
+ * head in tagged words.  Replaces, for K steps at once, the math_mpc loop
+ * body math_model_tree.py:515-635 (as mpc_episode_chain_step does per step).
  *   ws          mpc_episode_run_workspace_bytes(n_cand, n_steps); its polled
  *               part is zeroed on `stream` before the launch
  *   out         the LAST step's winner (re-rolled states)
