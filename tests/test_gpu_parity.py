@@ -649,3 +649,38 @@ def test_run_two_units_per_block_and_step(engine):
     ep.run(batches)
     assert _episode_log(ep) == want
     assert ep.chain_error() == 0
+
+
+@pytest.mark.parametrize("extra", [[], ["--integrator", "rect+rot"]])
+def test_bench_contract(extra):
+    """bench.py (a short run, no CPU leg) prints ONE JSON line with the
+    driver's contract keys; the default step is the chained rect+cum launch
+    and its roofline is the chained kernel's, with the committed PMC traffic
+    of that kernel; two-launch rect+rot reports the rollout kernel."""
+    import json
+    import os
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--steps", "8",
+                        "--warmup", "2", "--cpu-seconds", "0", "--no-second-pass"] + extra,
+                       capture_output=True, text=True, timeout=110, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 8 and d["warmup"] == 2 and d["value"] > 0
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] < 1
+    assert rf["algorithmic_bytes_per_launch"] == 16.0 * 10 * 1_000_000
+    if extra:
+        assert d["config"]["integrator"] == "rect+rot"
+        assert rf["kernel"] == "k_rollout_argmin_stream"
+    else:
+        assert d["config"]["integrator"] == "rect+cum"
+        assert rf["kernel"] == "k_episode_chain"
+        assert d["config"]["step_launches"].startswith("chained")
+    assert rf["traffic"] is not None and abs(rf["traffic"] / 160e6 - 1) < 0.01
