@@ -757,12 +757,124 @@ __device__ __forceinline__ void run_stream_wave(RunLds& sh, const double* const*
 #endif
 }
 
+// Block-wise streaming (MPC_RUN_BLOCKWISE): a streaming block rolls out one
+// unit after the other with the chained step's tile path (rollout_lane_glds_k,
+// 96 VGPRs: 5 waves/SIMD) — h speculated from the last head the block knows,
+// the unit's head polled three steps before its loop ends and waited for at
+// its end (the loop reruns with the final constants if h was wrong), then
+// the block's arg-min is the unit's record.  No quarters are held back: a
+// block waits at a unit's end until that step's head is out.
+template <int INTEG, bool PL2>
+__device__ __forceinline__ void run_stream_block(const double* const* __restrict__ ctl,
+                                                 int64_t total, int64_t T, int64_t s, int64_t G,
+                                                 int64_t n_cand, int n_steps,
+                                                 RunCtl* __restrict__ rc,
+                                                 uint64_t* __restrict__ rec,
+                                                 EpisodeState* __restrict__ S, double delta_t) {
+  constexpr int CPL = 2;
+  __shared__ uint32_t s_w[64];   // loop words of the head of step jk
+  const int q = threadIdx.x;
+  if (q < 64 && run_loop_word(q)) s_w[q] = reinterpret_cast<const uint32_t*>(&S->h)[q];
+  __syncthreads();
+  Consts K = consts_from_words(s_w);   // the head of step jk (the call's first: S->h)
+  double tk = run_words_t(s_w);
+  int64_t jk = 0;
+  const RunPubCopy& pubc = rc->copy[s % kRunPubCopies];
+  for (int64_t u = s; u < total; u += G) {
+    const int64_t j = u / T;
+    const int64_t tile = u - j * T;
+    const double* v = ctl[2 * j];
+    const double* b = ctl[2 * j + 1];
+    const int64_t c0 = tile * (kBlock * CPL) + q * CPL;
+    const int64_t cl = c0 < n_cand ? c0 : n_cand - CPL;
+    const bool have = jk == j;
+    Consts Kl, Kf;
+    uint64_t w_pre = 0;
+    bool pre_issued = false;
+    auto pre0 = [&]() {
+      Kl = K;
+      if (have) return;
+      double t = tk;   // + dt per step since, as episode_prepare forms it
+      for (int64_t r = jk; r < j; ++r) t = t + delta_t;
+      Kl.h = (t + delta_t) - t;
+    };
+    auto mid = [&]() {
+      if (have || pre_issued) return;
+      pre_issued = true;
+      if (q < 64 && run_loop_word(q)) w_pre = granule_load(pubc.pub[j & 1] + q);
+    };
+    auto wait = [&]() {
+      if (q == 0) RUN_UT(u, 1);
+      if (!have) {
+        __syncthreads();   // s_w reuse
+        if (q < 64) {
+          const uint32_t tag = static_cast<uint32_t>(j + 1);
+          bool fin = false;
+          if (pre_issued) {
+            const bool ok = !run_loop_word(q) || static_cast<uint32_t>(w_pre) == tag;
+            fin = __ballot(!ok) == 0;
+            if (fin && run_loop_word(q)) s_w[q] = static_cast<uint32_t>(w_pre >> 32);
+          }
+          for (uint32_t it = 0; !fin; ++it) {
+            fin = run_read_words(pubc.pub[j & 1], tag, s_w);
+            if (fin) break;
+            if (it >= kRunSpinLimit || run_aborted(rc)) {
+              if (q == 0) run_fail(rc, S, 2);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(4);
+          }
+        }
+        __syncthreads();
+        K = consts_from_words(s_w);
+        tk = run_words_t(s_w);
+        jk = j;
+      }
+      if (q == 0) RUN_UT(u, 2);
+      Kf = K;
+    };
+    if (q == 0) RUN_UT(u, 0);
+    double cst[CPL];
+    rollout_lane_glds_k<INTEG, kRotCum, PL2, decltype(wait), decltype(pre0), decltype(mid),
+                        false>(Kf, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0, mid);
+    uint64_t bk = ~0ull;
+    int64_t bi = INT64_MAX;
+    if (c0 < n_cand) {
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const uint64_t kk = cost_key(cst[c]);
+        if (kk < bk) {
+          bk = kk;
+          bi = c0 + c;
+        }
+      }
+    }
+    block_argmin(bk, bi);
+    if (q == 0) {
+      const uint32_t tag = static_cast<uint32_t>(j + 1);
+      uint64_t* r = rec + ((j & 1) * T + tile) * kRunRecWords;
+      granule_store(r, tag, static_cast<uint32_t>(bk >> 32));
+      granule_store(r + 1, tag, static_cast<uint32_t>(bk));
+      granule_store(r + 2, tag, static_cast<uint32_t>(bi));   // < 2^31 (host check)
+      RUN_UTV(u, 7, blockIdx.x);
+      RUN_UT(u, 3);
+    }
+  }
+}
+
 constexpr int kRunThreads = kBlock;   // 4 waves: the selector's, or a streaming block's
 // Launch bound: waves per SIMD (4 blocks of 4 waves per CU).  It must not ask
 // for more than LDS allows: that makes the bound void for the out-of-line
 // callees (run_rescore then took 180 VGPRs, 2 blocks per CU).
+#ifndef MPC_RUN_BLOCKWISE
+#define MPC_RUN_BLOCKWISE 1   // 0: run_stream_wave (wave-wise quarters kept in registers, 3 waves/SIMD)
+#endif
 #ifndef MPC_RUN_WAVES
+#if MPC_RUN_BLOCKWISE
+#define MPC_RUN_WAVES 5
+#else
 #define MPC_RUN_WAVES 3
+#endif
 #endif
 constexpr uint32_t kRunRegisterTicks = 1000;   // s_memrealtime (100 MHz): 10 us without a new block
 
@@ -787,7 +899,9 @@ __global__ __launch_bounds__(kRunThreads, MPC_RUN_WAVES) void k_episode_run(
   constexpr int CPL = 2;
   const int64_t T = (n_cand + kBlock * CPL - 1) / (kBlock * CPL);
   const int64_t total = T * k_steps;
+#if !MPC_RUN_BLOCKWISE
   __shared__ RunLds sh;
+#endif
   __shared__ uint32_t s_role, s_nres;
   if (threadIdx.x == 0) {
     const uint32_t r =
@@ -825,11 +939,13 @@ __global__ __launch_bounds__(kRunThreads, MPC_RUN_WAVES) void k_episode_run(
     s_role = r;
     s_nres = n;
   }
+#if !MPC_RUN_BLOCKWISE
   if (threadIdx.x < kRunSlots) {
     sh.cnt[threadIdx.x] = 0;
     sh.seq[threadIdx.x] = threadIdx.x;
   }
-  __syncthreads();   // the only barrier of a streaming block
+#endif
+  __syncthreads();
   const uint32_t role = s_role, nres = s_nres;
   if (role == 0u) {
     if (nres < 2u) return;
@@ -848,10 +964,16 @@ __global__ __launch_bounds__(kRunThreads, MPC_RUN_WAVES) void k_episode_run(
     return;
   }
   if (role >= nres) return;   // registered after the count was taken: no units
+#if MPC_RUN_BLOCKWISE
+  run_stream_block<INTEG, PL2>(ctl, total, T, static_cast<int64_t>(role) - 1,
+                               static_cast<int64_t>(nres) - 1, n_cand, n_steps, rc, rec, S,
+                               ecfg.delta_t);
+#else
   const Consts Kc = S->h.K;   // wheelbase terms (h set per unit)
   run_stream_wave<INTEG, PL2>(sh, ctl, total, T, static_cast<int64_t>(role) - 1,
                               static_cast<int64_t>(nres) - 1, n_cand, n_steps, rc, rec, S, Kc,
                               ecfg.delta_t);
+#endif
 }
 
 // Resident blocks of one run instantiation (occupancy x CUs), per device.
