@@ -21,7 +21,10 @@ import json,sys
 o='$OUT'
 w1=json.load(open(o+'/w1.json')); w2=json.load(open(o+'/w2.json')); w4=json.load(open(o+'/w4.json'))
 print('C steps', len(w1), len(w2), len(w4))
-print('C w2 identical:', w1 == w2, ' w4 identical:', w1 == w4)
+# one rank runs the chained kernel pass too (more real steps): compare the
+# steps all three logged
+n=min(len(w1), len(w2), len(w4))
+print('C w2 identical:', w1[:n] == w2[:n], ' w4 identical:', w1[:n] == w4[:n], ' over', n, 'steps')
 f1=json.load(open(o+'/f1.json')); f2=json.load(open(o+'/f2.json'))
 print('F steps', len(f1), len(f2), ' identical:', f1 == f2)
 " || true
