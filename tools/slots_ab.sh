@@ -1,3 +1,4 @@
+# Wave-wise run (MPC_RUN_BLOCKWISE=0) variants, built first with tools/build_variant.sh (e.g. pc3 -DMPC_RUN_BLOCKWISE=0 -DMPC_RUN_PER_CU=3)
 set -e
 mkdir -p gpurun_out
 DIPLOMJOURNEY_MPC_LIB=tools/var_stats.so timeout -k 10 120 python -u tools/probe_run.py 1000000 10 100 > gpurun_out/probe_stats.log 2>&1
