@@ -469,18 +469,20 @@ def run_persistent(args, ep, pool, world, device):
             "kernel_in_step_ms": e0.elapsed_time(e1) / K}
 
 
-def kernel_pass(ep, pool, reps=100):
+def kernel_pass(ep, pool, reps=100, warm=200):
     """The rollout kernel alone: REPS back-to-back launches between two HIP
     events on the launch stream, rotating over the resident batches (at least
     4 x the batch bytes between two uses of a batch, so no launch is served
     from the 256 MiB Infinity Cache; events around the single launch inside a
-    step would add their own packet overhead)."""
+    step would add their own packet overhead), after WARM untimed ones (see
+    chain_pass)."""
     import torch
     k0 = torch.cuda.Event(enable_timing=True)
     k1 = torch.cuda.Event(enable_timing=True)
     saved = ep.cur
-    ep.cur = pool[0]
-    ep.partials()
+    for i in range(warm + 1):
+        ep.cur = pool[i % len(pool)]
+        ep.partials()
     k0.record()
     for i in range(reps):
         ep.cur = pool[(i + 1) % len(pool)]
@@ -495,15 +497,18 @@ TRAFFIC_JSON = {"k_rollout_argmin_stream": "r02_traffic.json",
                 "k_episode_chain": "r02_traffic_chain.json"}
 
 
-def chain_pass(ep, pool, reps=100):
+def chain_pass(ep, pool, reps=100, warm=200):
     """The chained launch (rollout of step k + completion of step k-1): REPS
     back-to-back launches between two HIP events on the launch stream,
-    rotating over the resident batches as kernel_pass does; the episode goes
-    on (the launches are real steps)."""
+    rotating over the resident batches as kernel_pass does, after WARM
+    untimed ones (a short bench run, e.g. --steps 20, leaves the GPU's clocks
+    still ramping: 38 -> 34 us per launch over the first ~400); the episode
+    goes on (the launches are real steps)."""
     import torch
     k0 = torch.cuda.Event(enable_timing=True)
     k1 = torch.cuda.Event(enable_timing=True)
-    ep.step(controls=pool[0])
+    for i in range(warm + 1):
+        ep.step(controls=pool[i % len(pool)])
     k0.record()
     for i in range(reps):
         ep.step(controls=pool[(i + 1) % len(pool)])
