@@ -3,35 +3,29 @@
 //
 // Why: a step launched as its own kernel(s) pays, every step, the launch's
 // fill and drain (first control loads in flight with nothing to compute, the
-// last tiles finishing on a part-idle chip) and the one-block selection
-// during which HBM idles.  In kRotCum mode a candidate's rollout needs no
-// start pose (mpc_device.h step_start / cum_pose), so step j+1's candidates
-// can stream while step j is still being selected; only the final pose
-// transform and the criterion wait for the pose.  One launch streams the K
-// steps' tiles back to back:
+// last tiles finishing on a part-idle chip).  In kRotCum mode a candidate's
+// rollout needs no start pose (mpc_device.h step_start / cum_pose), so step
+// j+1's candidates can stream while step j is still being selected; only the
+// final pose transform and the criterion wait for the pose.  One launch
+// streams the K steps' tiles back to back:
 //
 //   unit u = (step j, tile) = (u / T, u % T), T = tiles of 512 candidates per
 //   step.  Blocks register in start order; the first one selects
 //   (run_select_step, one step after the other), the others stream units
 //   s, s + G, s + 2G, ... (streaming block s of G registered ones: every
 //   block that owns units is running, whatever residency the occupancy API
-//   promised).  A streaming block's 4 waves are independent (run_stream_wave):
-//   - each wave streams its quarter (128 candidates) of the block's units with
-//     an LDS-DMA control ring that runs ACROSS units (a unit's last steps
-//     already issue the next unit's first rows), the step size h speculated
-//     from the last head the wave knows (+ dt per step, as episode_prepare
-//     forms it);
-//   - at a unit's end it keeps the quarter's position sums in registers (up
-//     to kRunPend quarters) and goes on; it polls the oldest one's head with
-//     an LDS-DMA that lands behind its counted waits, then scores the quarter
-//     (the final pose transform and criterion; a mis-speculated h — an
-//     episode restart reset t — or an irregular candidate is re-rolled at the
-//     unit's end) and counts it in LDS; the wave whose count completes the
-//     unit writes its tagged record;
-//   - the selector sweeps step j's T records, re-rolls the winner
-//     (emit_winner), applies the episode update (episode_advance: finishing
-//     logic, operator events, restart, log record, the next step's t and
-//     constants) and publishes step j+1's head.
+//   promised).  A streaming block (run_stream_block) rolls out one unit at a
+//   time with the chained step's tile path (rollout_lane_glds_k, 5
+//   waves/SIMD), the step size h speculated from the last head it knows (+ dt
+//   per step, as episode_prepare forms it); it polls the unit's head three
+//   steps before the loop ends, waits for it at the end (the loop reruns with
+//   the final constants if h was wrong), and its arg-min is the unit's tagged
+//   record.  The selector sweeps step j's T records, re-rolls the winner
+//   (emit_winner), applies the episode update (episode_advance: finishing
+//   logic, operator events, restart, log record, the next step's t and
+//   constants) and publishes step j+1's head.
+//   (Measured: level with the chained steps of mpc_episode_chain_step at 8e6
+//   candidates per step, slower at 1e6 — DESIGN.md §6d.)
 //
 // Hand-offs (MI355X_MICROARCH.md "inter-workgroup visibility",
 // cdna_hip_programming.md Guideline 16 R2): every handed-off word is an 8-byte
@@ -161,41 +155,6 @@ __device__ __forceinline__ double run_words_t(const uint32_t* s_w) {
   return __longlong_as_double(static_cast<long long>((hi << 32) | lo));
 }
 
-// Consts from head granules (data in the high 32 bits), field by field.
-__device__ __forceinline__ Consts consts_from_granules(const uint64_t* g) {
-  auto d = [&](size_t off) {
-    const int q = static_cast<int>(off / 4);
-    const uint64_t lo = static_cast<uint32_t>(
-        __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(g[q] >> 32)));
-    const uint64_t hi = static_cast<uint32_t>(
-        __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(g[q + 1] >> 32)));
-    return __longlong_as_double(static_cast<long long>((hi << 32) | lo));
-  };
-  Consts K;
-  K.x = d(offsetof(Consts, x));
-  K.y = d(offsetof(Consts, y));
-  K.phi = d(offsetof(Consts, phi));
-  K.x_t = d(offsetof(Consts, x_t));
-  K.y_t = d(offsetof(Consts, y_t));
-  K.x_0 = d(offsetof(Consts, x_0));
-  K.y_0 = d(offsetof(Consts, y_0));
-  K.A = d(offsetof(Consts, A));
-  K.B = d(offsetof(Consts, B));
-  K.C1 = d(offsetof(Consts, C1));
-  K.C2 = d(offsetof(Consts, C2));
-  K.den = d(offsetof(Consts, den));
-  K.L = d(offsetof(Consts, L));
-  K.inv_L = d(offsetof(Consts, inv_L));
-  K.h = d(offsetof(Consts, h));
-  K.hlgth = d(offsetof(Consts, hlgth));
-  K.s0 = d(offsetof(Consts, s0));
-  K.c0 = d(offsetof(Consts, c0));
-  K.L_pow2 = static_cast<int32_t>(__builtin_amdgcn_readfirstlane(
-      static_cast<uint32_t>(g[offsetof(Consts, L_pow2) / 4] >> 32)));
-  K.pad_ = 0;
-  return K;
-}
-
 // Step j's T unit records (kRunRecWords granules each, tag j + 1) -> the
 // lexicographic (cost key, local index) minimum, per thread (the caller
 // reduces over the block).  Every thread sweeps its records kSw at a time, all
@@ -288,10 +247,10 @@ __device__ __noinline__ void run_select_step(
   const bool last = j + 1 == k_steps;
   uint64_t k;
   int64_t i;
-  const uint64_t t0 = RUN_TICK();
+  [[maybe_unused]] const uint64_t t0 = RUN_TICK();
   run_sweep_records(rec + (j & 1) * T * kRunRecWords, T, tag, rc, S, k, i);
   block_argmin(k, i);   // (its barrier also orders the head's LDS words)
-  const uint64_t t1 = RUN_TICK();
+  [[maybe_unused]] const uint64_t t1 = RUN_TICK();
   if (q == 0) RUN_TL_MAX(j, 3);
   Winner w;
   {
@@ -300,7 +259,7 @@ __device__ __noinline__ void run_select_step(
     __builtin_memcpy(&inc, &s_head[offsetof(EpisodeHead, incumbent) / 4], sizeof(double));
     emit_winner<INTEG, kRotCum>(Kj, v, b, n_cand, n_steps, k, i, index_base + i, inc, res, &w);
   }
-  const uint64_t t2 = RUN_TICK();
+  [[maybe_unused]] const uint64_t t2 = RUN_TICK();
   if (q == 0) {   // emit_winner ended with a barrier
     EpisodeHead H;
     __builtin_memcpy(&H, s_head, sizeof(EpisodeHead));
@@ -317,7 +276,7 @@ __device__ __noinline__ void run_select_step(
   if (clock && q == 0) clock[j] = __builtin_amdgcn_s_memrealtime();
   if (q == 0) RUN_TL_MAX(j, 4);
   if (q == 0) {
-    const uint64_t t3 = RUN_TICK();
+    [[maybe_unused]] const uint64_t t3 = RUN_TICK();
     RUN_STAT(8, t1 - t0);
     RUN_STAT(9, t2 - t1);
     RUN_STAT(10, t3 - t2);
@@ -330,434 +289,7 @@ __device__ __noinline__ void run_select_step(
   __syncthreads();   // s_log / s_slot reuse
 }
 
-// Per streaming block: the quarter minima of its units (unit k in slot
-// k % kRunSlots) and each wave's head-poll buffer.  LDS only; the four
-// streaming waves order their accesses with lgkmcnt waits (LDS operations of
-// a wave complete in order) and relaxed LDS atomics.  A wave keeps its own
-// unscored quarters (position sums) in registers: no parking in LDS, which
-// left room for 4 blocks a CU.
-#ifndef MPC_RUN_SLOTS
-#define MPC_RUN_SLOTS 4
-#endif
-constexpr int kRunSlots = MPC_RUN_SLOTS;   // minima slots per block (unit k in slot k % kRunSlots)
-static_assert(kRunSlots >= 1 && kRunSlots <= 8, "MPC_RUN_SLOTS must be in [1, 8]");
-// The run's own control ring (kRunRing - 1 steps in flight per wave).  (4
-// slots: 54272 B of LDS a block, and only 2 blocks per CU became resident.)
-#ifndef MPC_RUN_RING
-#define MPC_RUN_RING 4
-#endif
-constexpr int kRunRing = MPC_RUN_RING;
-static_assert(kRunRing >= 2 && kRunRing <= 4, "MPC_RUN_RING must be in [2, 4]");
-__shared__ double2 g_run_ring[kWaves][kRunRing][2][64];  // [wave][slot][v|beta][lane]
-struct RunLds {
-  uint64_t qkey[kRunSlots][kWaves]; // each wave's quarter minimum
-  int64_t qidx[kRunSlots][kWaves];
-  int32_t cnt[kRunSlots];           // quarters of the slot's unit scored
-  int32_t seq[kRunSlots];           // unit index (per block) the slot accepts next
-  uint64_t poll[kWaves][64];        // each wave's head poll (LDS-DMA target)
-};
-
-__device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
-// 16 bytes (two granules) of a published head into this lane's 16 bytes of
-// the LDS buffer at dst (lanes 0-31: 64 granules), bypassing the non-coherent
-// cache levels (sc1, as an agent-scope relaxed load).  Counted by vmcnt like
-// the control rows; the caller orders earlier LDS reads of the buffer first.
-__device__ __forceinline__ void glds_poll(const uint64_t* g, uint32_t dst) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off sc1\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(g), "s"(dst)
-      : "memory");
-}
-
-__device__ __forceinline__ int32_t lds_load(const int32_t* p) {
-  return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_store(int32_t* p, int32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// One wave: the unit's four quarter minima (LDS) -> unit u's record (step j,
-// tag j + 1); then the slot is free for the block's unit k + kRunSlots.
-__device__ __forceinline__ void run_combine(RunLds& sh, uint64_t* __restrict__ rec, int64_t T,
-                                            int sl, int32_t k, int64_t u, int64_t j) {
-  const int lane = threadIdx.x & 63;
-  uint64_t bk = ~0ull;
-  int64_t bi = INT64_MAX;
-#pragma unroll
-  for (int w = 0; w < kWaves; ++w) {
-    const uint64_t k2 = sh.qkey[sl][w];
-    const int64_t i2 = sh.qidx[sl][w];
-    if (rec_less(k2, i2, bk, bi)) {
-      bk = k2;
-      bi = i2;
-    }
-  }
-  if (lane == 0) {
-    const uint32_t tag = static_cast<uint32_t>(j + 1);
-    uint64_t* r = rec + ((j & 1) * T + (u - j * T)) * kRunRecWords;
-    granule_store(r, tag, static_cast<uint32_t>(bk >> 32));
-    granule_store(r + 1, tag, static_cast<uint32_t>(bk));
-    granule_store(r + 2, tag, static_cast<uint32_t>(bi));   // < 2^31 (host check)
-    RUN_UT(u, 3);
-    lds_store(&sh.cnt[sl], 0);
-    lds_order();
-    lds_store(&sh.seq[sl], k + kRunSlots);
-  }
-}
-
-// The rare path of scoring a parked candidate (out of line: it must not cost
-// the streaming loop registers): a mis-speculated step size (an episode
-// restart reset t) re-rolls the candidate from its controls with the head's
-// h; an irregular candidate re-runs the safe recurrence; otherwise the
-// parked sums give the pose.  `head`: the step's head granules (LDS).
-template <int INTEG, bool PL2>
-__device__ __noinline__ uint64_t run_rescore(const uint64_t* head, double hq, const double* cv,
-                                             const double* cb, int64_t n_cand, int n_steps,
-                                             int64_t col, double a, double b, bool irregular) {
-  const Consts K = consts_from_granules(head);
-  double cst;
-  if (hq != K.h) {
-    cst = rollout_candidate_l<INTEG, kRotCum, PL2>(K, cv, cb, n_cand, col, n_steps, nullptr);
-  } else if (irregular) {
-    double xx = K.x, yy = K.y, ph = K.phi;
-    for (int sr = 0; sr < n_steps; ++sr)
-      step_safe<INTEG>(xx, yy, ph, cv[sr * n_cand + col], cb[sr * n_cand + col], K);
-    cst = cost(xx, yy, K);
-  } else {
-    double xx, yy;
-    cum_pose(K, a, b, xx, yy);
-    cst = cost(xx, yy, K);
-  }
-  return cost_key(cst);
-}
-
-// A wave's unscored quarter: its lanes' position sums and irregular flags,
-// the h its loop used, the block's unit index and the step.
-struct RunPend {
-  double2 a, b;   // (A0, A1), (B0, B1)
-  uint32_t bad;   // bit c: candidate c irregular
-  double h;
-  int32_t k;
-  int64_t j;
-};
-#ifndef MPC_RUN_PEND
-#define MPC_RUN_PEND 2
-#endif
-constexpr int kRunPend = MPC_RUN_PEND;   // unscored quarters a wave holds (registers)
-static_assert(kRunPend >= 1 && kRunPend <= 4, "MPC_RUN_PEND must be in [1, 4]");
-
-// Streaming wave (waves 0-3 of a streaming block): rolls out its quarter (128
-// candidates: lane l of wave w holds candidates tile*512 + (64w + l)*2 + {0,1})
-// of each of the block's units (s, s + G, s + 2G, ... for streaming block s of
-// G), keeps the sums in registers and goes on.  The control ring (kRing slots of one step's
-// v and beta rows, kRing-1 steps in flight) continues across units.  The
-// wave learns a parked quarter's head by polling it with an LDS-DMA into its
-// own buffer (it lands behind the counted waits two steps later), scores the
-// quarter and counts it; the wave whose count completes the unit combines the
-// four minima into the unit's record and frees the slot.  The only blocking
-// waits: its own control rows; at a unit's end, when the wave already holds
-// kRunPend unscored quarters, the oldest one's head; and a minima slot still
-// holding the unit kRunSlots before (another wave that far behind).
-template <int INTEG, bool PL2>
-__device__ __forceinline__ void run_stream_wave(RunLds& sh, const double* const* __restrict__ ctl,
-                                                int64_t total, int64_t T, int64_t s, int64_t G,
-                                                int64_t n_cand, int n_steps,
-                                                RunCtl* __restrict__ rc,
-                                                uint64_t* __restrict__ rec,
-                                                EpisodeState* __restrict__ S, const Consts& Kc,
-                                                double delta_t) {
-  constexpr int CPL = 2;
-  constexpr int R = kRunRing;
-  constexpr uint32_t kSlot = 2 * 64 * sizeof(double2);   // 2 KiB: v and beta rows
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t ring0 = __builtin_amdgcn_readfirstlane(lds_addr(&g_run_ring[wv][0][0][0]));
-  auto dst = [&](uint32_t slot) { return ring0 + slot * kSlot; };
-  auto unit_of = [&](int32_t k) -> int64_t {   // the block's k-th unit
-    const int64_t u = s + static_cast<int64_t>(k) * G;
-    return u < total ? u : total;
-  };
-  auto lane_col = [&](int64_t tile) {
-    const int64_t c0 = tile * (kBlock * CPL) + threadIdx.x * CPL;
-    return c0 < n_cand ? c0 : n_cand - CPL;   // lanes past a partial tile repeat the last pair
-  };
-  int64_t u = unit_of(0);
-  if (u >= total) return;
-  // issue cursor: the block's ik-th unit iu = (step ij, tile itile), control row ist
-  int32_t ik = 0;
-  int64_t iu = u, ij = u / T, itile = u - (u / T) * T;
-  int ist = 0;
-  const double* iv = ctl[2 * ij];
-  const double* ib = ctl[2 * ij + 1];
-  int64_t icl = lane_col(itile);
-  uint32_t gi = 0, gc = 0;              // control rows issued / consumed (ring slot = count % R)
-  auto issue = [&](bool dep, const double2& rv, const double2& rb) -> bool {
-    if (iu >= total) return false;
-    const uint32_t sl = gi % R;
-    if (dep)
-      glds_refill(iv + ist * n_cand + icl, ib + ist * n_cand + icl, dst(sl), dst(sl) + kSlot / 2,
-                  rv, rb);
-    else
-      glds_pair(iv + ist * n_cand + icl, ib + ist * n_cand + icl, dst(sl), dst(sl) + kSlot / 2);
-    ++gi;
-    if (++ist == n_steps) {
-      ist = 0;
-      iu = unit_of(++ik);
-      if (iu < total) {
-        ij = iu / T;
-        itile = iu - ij * T;
-        iv = ctl[2 * ij];
-        ib = ctl[2 * ij + 1];
-        icl = lane_col(itile);
-      }
-    }
-    return true;
-  };
-  {
-    const double2 z = make_double2(0.0, 0.0);
-#pragma unroll
-    for (int q = 0; q < R - 1; ++q) issue(false, z, z);
-  }
-  double2 rv = make_double2(0.0, 0.0), rb = rv;   // the slot read last (refill dependency)
-  trig::Leads lead = trig::const_leads();
-  Consts Kl = Kc;                        // wheelbase terms; h per unit
-#ifdef MPC_RUN_STATS
-  uint64_t st_acc[16] = {0};
-#endif
-  // This wave's unscored quarters, oldest first (e0, then e1).
-  const uint32_t pollw = __builtin_amdgcn_readfirstlane(lds_addr(&sh.poll[wv][0]));
-  const RunPubCopy& pubc = rc->copy[s % kRunPubCopies];
-  int pend_n = 0;
-  RunPend e0{}, e1{}, e2{}, e3{};   // (entries past kRunPend are never used)
-  int64_t khj = 0;                       // latest step whose head this wave took (poll buffer)
-  double kt = S->h.t;                    // that head's t (the speculation's base)
-  int poll_age = 0;                      // 0: none in flight; else steps waited since issue
-  int64_t poll_j = 0;
-  {
-    // the call's first head, as if polled (tag 1 = step 0)
-    const int q = lane;
-    const uint32_t w = run_loop_word(q) ? reinterpret_cast<const uint32_t*>(&S->h)[q] : 0u;
-    sh.poll[wv][q] = (static_cast<uint64_t>(w) << 32) | 1u;
-  }
-  auto head_t = [&]() {
-    const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
-        static_cast<uint32_t>(sh.poll[wv][kRunTDword] >> 32)));
-    const uint64_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
-        static_cast<uint32_t>(sh.poll[wv][kRunTDword + 1] >> 32)));
-    return __longlong_as_double(static_cast<long long>((hi << 32) | lo));
-  };
-  // score the oldest pending quarter with the head in the poll buffer (step
-  // e0.j).  Inside the streaming loop (slow = false) only the regular case:
-  // the rescoring call there cost the loop its registers (5x slower steps);
-  // it returns false and the quarter waits for the unit's end.
-  auto resolve_oldest = [&](bool slow) -> bool {
-    const int sl = e0.k % kRunSlots;
-    const int64_t u0 = unit_of(e0.k);
-    const int64_t pj0 = e0.j;
-    const double ph0 = e0.h;
-    const double tj = head_t();
-    const bool hok = ((tj + delta_t) - tj) == ph0;
-    const uint32_t bb = e0.bad;
-    const double2 px = e0.a, py = e0.b;
-    const int64_t c0 = (u0 - pj0 * T) * (kBlock * CPL) + threadIdx.x * CPL;
-    uint64_t k0, k1;
-    const bool regular = hok && __ballot(bb != 0u) == 0;
-    if (!slow && !regular) return false;
-    if (regular) {
-      const Consts K = consts_from_granules(sh.poll[wv]);
-      double xx, yy;
-      cum_pose(K, px.x, py.x, xx, yy);
-      k0 = cost_key(cost(xx, yy, K));
-      cum_pose(K, px.y, py.y, xx, yy);
-      k1 = cost_key(cost(xx, yy, K));
-    } else {
-      RUN_ACC(1, 1);
-      const int64_t cl = c0 < n_cand ? c0 : n_cand - CPL;
-      const double* cv = ctl[2 * pj0];
-      const double* cb = ctl[2 * pj0 + 1];
-      k0 = run_rescore<INTEG, PL2>(sh.poll[wv], ph0, cv, cb, n_cand, n_steps, cl, px.x, py.x,
-                                   (bb & 1u) != 0u);
-      k1 = run_rescore<INTEG, PL2>(sh.poll[wv], ph0, cv, cb, n_cand, n_steps, cl + 1, px.y, py.y,
-                                   (bb & 2u) != 0u);
-    }
-    uint64_t dk = ~0ull;
-    int64_t di = INT64_MAX;
-    if (c0 < n_cand) {
-      dk = k0;
-      di = c0;
-    }
-    if (c0 + 1 < n_cand && k1 < dk) {
-      dk = k1;
-      di = c0 + 1;
-    }
-    wave_argmin(dk, di);
-    // the slot still holds unit k - kRunSlots if another wave is that far behind
-    for (uint32_t it = 0; lds_load(&sh.seq[sl]) != e0.k; ++it) {
-      RUN_ACC(4, 1);
-      if ((it & 1023) == 1023 && run_aborted(rc)) break;
-      if (it >= kRunSpinLimit * 8u) {
-        if (lane == 0) run_fail(rc, S, 4);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    if (lane == 0) {
-      sh.qkey[sl][wv] = dk;
-      sh.qidx[sl][wv] = di;
-    }
-    lds_order();   // the minimum is in LDS before the count says so
-    int32_t prev = 0;
-    if (lane == 0)
-      prev = __hip_atomic_fetch_add(&sh.cnt[sl], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    prev = __builtin_amdgcn_readfirstlane(prev);
-    if (prev == kWaves - 1) {
-      lds_order();
-      run_combine(sh, rec, T, sl, e0.k, u0, pj0);
-    }
-    --pend_n;
-    e0 = e1;   // shift (static registers; entries past pend_n are don't-care)
-    if constexpr (kRunPend > 2) e1 = e2;
-    if constexpr (kRunPend > 3) e2 = e3;
-    return true;
-  };
-  // after a poll has landed: take it if every loop word carries the tag
-  auto take_poll = [&]() {
-    const int q = lane;
-    const uint64_t w = sh.poll[wv][q];
-    const bool ok =
-        !run_loop_word(q) || static_cast<uint32_t>(w) == static_cast<uint32_t>(poll_j + 1);
-    if (__ballot(!ok) == 0) {
-      khj = poll_j;
-      kt = head_t();
-    }
-    poll_age = 0;
-    while (pend_n > 0 && khj == e0.j && resolve_oldest(false)) {
-    }
-  };
-  // blocking: the head of the oldest pending quarter (relaxed polls)
-  auto wait_oldest = [&]() {
-    const uint64_t* g = pubc.pub[e0.j & 1];
-    const uint32_t tag = static_cast<uint32_t>(e0.j + 1);
-    const uint64_t w0 = RUN_TICK();
-    for (uint32_t it = 0;; ++it) {
-      const uint64_t w = run_loop_word(lane) ? granule_load(g + lane) : 0ull;
-      const bool ok = !run_loop_word(lane) || static_cast<uint32_t>(w) == tag;
-      if (__ballot(!ok) == 0) {
-        sh.poll[wv][lane] = w;
-        break;
-      }
-      if (it >= kRunSpinLimit || run_aborted(rc)) {
-        if (lane == 0) run_fail(rc, S, 2);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(4);
-    }
-    lds_order();
-    khj = e0.j;
-    kt = head_t();
-    poll_age = 0;
-    RUN_ACC(5, 1);
-    RUN_ACC(6, RUN_TICK() - w0);
-    while (pend_n > 0 && khj == e0.j) resolve_oldest(true);
-  };
-  for (int32_t k = 0; u < total; ++k, u = unit_of(k)) {
-    const int64_t j = u / T;
-    // step size: from this wave's latest head, + dt per step since
-    {
-      double t = kt;
-      for (int64_t q = khj; q < j; ++q) t = t + delta_t;
-      Kl.h = (t + delta_t) - t;          // consts_from_problem: t_b - t_a
-    }
-    double x[CPL], y[CPL], sn[CPL], cs[CPL];
-    bool bad[CPL];
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) {
-      double ph;
-      step_start<kRotCum>(Kl, x[q], y[q], ph, sn[q], cs[q]);
-      bad[q] = false;
-    }
-    if (lane == 0 && wv == 0) {
-      RUN_UT(u, 0);
-      RUN_UTV(u, 7, blockIdx.x);
-    }
-#pragma unroll 1
-    for (int st = 0; st < n_steps; ++st) {
-      issue(true, rv, rb);
-      const uint32_t ahead = gi - gc - 1;   // row pairs issued behind this one
-      static_assert(R <= 4, "tail waits below cover up to 3 pairs behind");
-      if (ahead >= R - 1)
-        wait_vm<2 * (R - 1)>();
-      else if (ahead == 2)
-        wait_vm<4>();
-      else if (ahead == 1)
-        wait_vm<2>();
-      else
-        wait_vm<0>();
-      const uint32_t sl = gc % R;
-      rv = g_run_ring[wv][sl][0][lane];
-      rb = g_run_ring[wv][sl][1][lane];
-      ++gc;
-      // (the heading itself is not carried: kRotCum rotates (sn, cs))
-      double h0 = 0.0, h1 = 0.0;
-      step_core<INTEG, kRotCum, PL2>(x[0], y[0], h0, sn[0], cs[0], rv.x, rb.x, Kl, bad[0], &lead);
-      step_core<INTEG, kRotCum, PL2>(x[1], y[1], h1, sn[1], cs[1], rv.y, rb.y, Kl, bad[1], &lead);
-      // the head poll of the oldest pending quarter: issued here, landed R-1
-      // counted waits later (R-1 more row pairs issued behind it), then taken
-      if (poll_age > 0 && ++poll_age >= R) take_poll();
-      if (pend_n > 0 && poll_age == 0) {
-        poll_j = e0.j;
-        lds_order();   // this wave's reads of the previous poll are done
-        if (lane < 32) glds_poll(pubc.pub[e0.j & 1] + 2 * lane, pollw);
-        poll_age = 1;
-      }
-    }
-    if (lane == 0 && wv == 0) RUN_UT(u, 1);
-    // a full hand: the oldest quarter's head first
-    if (pend_n == kRunPend) {
-      if (poll_age > 0) wait_vm<0>();    // (an in-flight poll must land first)
-      poll_age = 0;
-      wait_oldest();
-    }
-    if (lane == 0 && wv == 0) RUN_UT(u, 2);
-    {
-      RunPend e;
-      e.a = make_double2(x[0], x[1]);
-      e.b = make_double2(y[0], y[1]);
-      e.bad = (bad[0] ? 1u : 0u) | (bad[1] ? 2u : 0u);
-      e.h = Kl.h;
-      e.k = k;
-      e.j = j;
-      if (pend_n == 0)
-        e0 = e;
-      else if (kRunPend == 2 || pend_n == 1)
-        e1 = e;
-      else if (kRunPend == 3 || pend_n == 2)
-        e2 = e;
-      else
-        e3 = e;
-      ++pend_n;
-    }
-    // this wave already holds the head of its oldest pending step: score now
-    while (pend_n > 0 && khj == e0.j) resolve_oldest(true);
-  }
-  if (poll_age > 0) wait_vm<0>();
-  while (pend_n > 0) wait_oldest();   // the wave's last quarters
-#ifdef MPC_RUN_STATS
-  if (lane == 0)
-    for (int q = 0; q < 16; ++q)
-      if (st_acc[q]) RUN_STAT(q, st_acc[q]);
-#endif
-}
-
-// Block-wise streaming (MPC_RUN_BLOCKWISE): a streaming block rolls out one
+// Block-wise streaming: a streaming block rolls out one
 // unit after the other with the chained step's tile path (rollout_lane_glds_k,
 // 96 VGPRs: 5 waves/SIMD) — h speculated from the last head the block knows,
 // the unit's head polled three steps before its loop ends and waited for at
@@ -863,18 +395,11 @@ __device__ __forceinline__ void run_stream_block(const double* const* __restrict
 }
 
 constexpr int kRunThreads = kBlock;   // 4 waves: the selector's, or a streaming block's
-// Launch bound: waves per SIMD (4 blocks of 4 waves per CU).  It must not ask
-// for more than LDS allows: that makes the bound void for the out-of-line
-// callees (run_rescore then took 180 VGPRs, 2 blocks per CU).
-#ifndef MPC_RUN_BLOCKWISE
-#define MPC_RUN_BLOCKWISE 1   // 0: run_stream_wave (wave-wise quarters kept in registers, 3 waves/SIMD)
-#endif
+// Launch bound: waves per SIMD (5: the tile path's 96 VGPRs).  It must not ask
+// for more than LDS allows (that makes the bound void for the out-of-line
+// selector call).
 #ifndef MPC_RUN_WAVES
-#if MPC_RUN_BLOCKWISE
 #define MPC_RUN_WAVES 5
-#else
-#define MPC_RUN_WAVES 3
-#endif
 #endif
 constexpr uint32_t kRunRegisterTicks = 1000;   // s_memrealtime (100 MHz): 10 us without a new block
 
@@ -899,9 +424,6 @@ __global__ __launch_bounds__(kRunThreads, MPC_RUN_WAVES) void k_episode_run(
   constexpr int CPL = 2;
   const int64_t T = (n_cand + kBlock * CPL - 1) / (kBlock * CPL);
   const int64_t total = T * k_steps;
-#if !MPC_RUN_BLOCKWISE
-  __shared__ RunLds sh;
-#endif
   __shared__ uint32_t s_role, s_nres;
   if (threadIdx.x == 0) {
     const uint32_t r =
@@ -939,12 +461,6 @@ __global__ __launch_bounds__(kRunThreads, MPC_RUN_WAVES) void k_episode_run(
     s_role = r;
     s_nres = n;
   }
-#if !MPC_RUN_BLOCKWISE
-  if (threadIdx.x < kRunSlots) {
-    sh.cnt[threadIdx.x] = 0;
-    sh.seq[threadIdx.x] = threadIdx.x;
-  }
-#endif
   __syncthreads();
   const uint32_t role = s_role, nres = s_nres;
   if (role == 0u) {
@@ -964,16 +480,9 @@ __global__ __launch_bounds__(kRunThreads, MPC_RUN_WAVES) void k_episode_run(
     return;
   }
   if (role >= nres) return;   // registered after the count was taken: no units
-#if MPC_RUN_BLOCKWISE
   run_stream_block<INTEG, PL2>(ctl, total, T, static_cast<int64_t>(role) - 1,
                                static_cast<int64_t>(nres) - 1, n_cand, n_steps, rc, rec, S,
                                ecfg.delta_t);
-#else
-  const Consts Kc = S->h.K;   // wheelbase terms (h set per unit)
-  run_stream_wave<INTEG, PL2>(sh, ctl, total, T, static_cast<int64_t>(role) - 1,
-                              static_cast<int64_t>(nres) - 1, n_cand, n_steps, rc, rec, S, Kc,
-                              ecfg.delta_t);
-#endif
 }
 
 // Resident blocks of one run instantiation (occupancy x CUs), per device.

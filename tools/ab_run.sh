@@ -1,6 +1,6 @@
 # A/B of the persistent run variants against the per-step launch paths (one GPU box call).
 #   bash tools/ab_run.sh "variant ..."   (tools/var_<variant>.so; "default" = the in-tree library)
-# Variants first: bash tools/build_variant.sh NAME -D... (e.g. wavewise -DMPC_RUN_BLOCKWISE=0, stats -DMPC_RUN_STATS)
+# Variants first: bash tools/build_variant.sh NAME -D... (e.g. stats -DMPC_RUN_STATS; the wave-wise design is in the history: commit 50b37c6)
 set -e
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "run_" > gpurun_out/ab_tests.log 2>&1

@@ -1,5 +1,5 @@
 # Block-wise persistent run (tools/var_bw.so) vs the in-tree run and the chained default.
-# Variants first: bash tools/build_variant.sh bw -DMPC_RUN_BLOCKWISE=1; bash tools/build_variant.sh bwstats -DMPC_RUN_BLOCKWISE=1 -DMPC_RUN_STATS
+# Variants first: bash tools/build_variant.sh bw (the in-tree source); bash tools/build_variant.sh bwstats -DMPC_RUN_STATS
 set -e
 mkdir -p gpurun_out
 DIPLOMJOURNEY_MPC_LIB=tools/var_bw.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "run_" > gpurun_out/bw_tests.log 2>&1

@@ -14,9 +14,7 @@ from diplomjourney_amd import math_model_tree as mmt, native  # noqa: E402
 from diplomjourney_amd.episode import DeviceEpisode  # noqa: E402
 from diplomjourney_amd.expansion import Expansion  # noqa: E402
 
-NAMES = {1: "quarters re-rolled at a unit's end", 4: "minima-slot spins",
-         5: "full-hand waits (wave x unit)", 6: "full-hand wait ticks (sum over waves)",
-         8: "selector ticks sweep", 9: "selector ticks emit", 10: "selector ticks advance+pub",
+NAMES = {8: "selector ticks sweep", 9: "selector ticks emit", 10: "selector ticks advance+pub",
          11: "sweep polls", 31: "registered blocks (summed over launches)"}
 
 
@@ -54,7 +52,7 @@ def main():
     per = [(b - a) * 10e-3 for a, b in zip(c, c[1:])]
     per.sort()
     print(f"n={n} ns={ns} K={K}: {dt / K * 1e6:.1f} us/step wall, period p50 {per[len(per) // 2]:.1f} us")
-    u = max(1, st[5])
+    u = 1
     for i, name in NAMES.items():
         extra = ""
         if "ticks" in name and "selector" not in name:
