@@ -99,7 +99,7 @@ def parse():
     ap.add_argument("--host-loop", action="store_true",
                     help="drive the episode from the host (one 808-B read + host update per "
                          "step) instead of the device-resident episode")
-    ap.add_argument("--inputs", default="resident", choices=["resident", "sampled"],
+    ap.add_argument("--inputs", default="resident", choices=["resident", "sampled", "generated"],
                     help="resident: each step's candidates already in HBM (the contract's "
                          "input); sampled: the device sampler regenerates them per step")
     ap.add_argument("--no-second-pass", action="store_true",
@@ -229,7 +229,8 @@ def main():
         ep = DeviceEpisode(eng, n_total, n_steps, rank=rank, world=world,
                            integrator=args.integrator, group=group, log_capacity=8192,
                            exchange=exchange, split=not args.fused,
-                           chain=not args.no_chain and args.integrator == "rect+cum")
+                           chain=not args.no_chain and args.integrator == "rect+cum",
+                           generate=inputs == "generated")
     pool = make_pool(eng, ep, n_steps, args.steps) if inputs == "resident" else None
     persistent = args.run
     # the launch that carries the step: the chained kernel (rollout of step k +
@@ -251,10 +252,12 @@ def main():
         kern_ms = main_run["kernel_in_step_ms"]
         if chained:
             kern_ms = chain_pass(ep, pool)
+        elif inputs == "generated":
+            pass   # events around the generated rollout + selection (no HBM roofline)
         elif hasattr(ep, "partials"):
             kern_ms = kernel_pass(ep, pool if pool is not None else
                                   make_pool(eng, ep, n_steps, 4))
-    other = None
+    other = generated = None
     if not args.host_loop and not args.no_second_pass:
         # the other input mode, same episode machinery, for comparison
         other_pool = None if inputs == "resident" else make_pool(eng, ep, n_steps, args.steps)
@@ -263,6 +266,14 @@ def main():
                  "value": n_total * args.steps / r["elapsed"],
                  "ms_per_step": r["elapsed"] / args.steps * 1e3, "p50_ms": r["p50_ms"]}
         del other_pool
+        if inputs == "resident" and not exchange:
+            # the sampled candidates drawn inside the rollout instead (one GPU)
+            ep.generate = True
+            r = run_steps(args, ep, None, use_graph, world, device)
+            ep.generate = False
+            generated = {"inputs": "generated", "value": n_total * args.steps / r["elapsed"],
+                         "ms_per_step": r["elapsed"] / args.steps * 1e3,
+                         "p50_ms": r["p50_ms"]}
     elapsed = main_run["elapsed"]
     bytes_launch = 16.0 * n_steps * ep.n_local * (args.steps if persistent else 1)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
@@ -310,8 +321,10 @@ def main():
                      "(selection published) inside the timed persistent launch" if persistent else
                      "GPU time per MPC step (HIP events between step starts, eager launches)"),
         "kernel_ms": kern_ms, "kernel_in_step_ms": main_run["kernel_in_step_ms"],
-        "roofline": roofline(achieved, bytes_launch, args.traffic_json, kernel=kernel),
+        "roofline": (None if inputs == "generated" else
+                     roofline(achieved, bytes_launch, args.traffic_json, kernel=kernel)),
         "other_inputs": other,
+        "generated_inputs": generated,
         "cpu_baseline": cpu,
     }
     if rank == 0:
@@ -328,6 +341,9 @@ INPUTS_DOC = {
     "sampled": "per step the device sampler regenerates the candidates on the grid around "
                "the episode's current control (the reference's per-step grid); the step = "
                "sampler + rollout/arg-min + finalize/episode update",
+    "generated": "the sampled mode's candidates drawn inside the rollout kernel (grid in LDS, "
+                 "the sampler's hash per candidate-step; never written to HBM); the step = "
+                 "generated rollout/arg-min + finalize/episode update",
 }
 
 

@@ -177,6 +177,133 @@ __global__ __launch_bounds__(kBlock) void k_episode_sample(
   sample_items(s_grid, n_grid, n_cand, n_steps, seed, base, 1, v, b, n_cand, pairs);
 }
 
+// ---------------------------------------------------------------------------
+// Generated controls (inputs "generated", mpc_episode_generate_step): the
+// sampler of k_episode_sample and the rollout of k_rollout_argmin_stream in
+// ONE kernel — every block builds the step's grid (episode_grids) in LDS and
+// each lane draws its candidates' (v, beta) per step from it with the same
+// splitmix64 -> multiply-shift map (grid_entry, constant prefix included),
+// so the controls never touch HBM.  Per lane two candidates, the same
+// operations in the same order as the streaming kernel's lane
+// (rollout_lane_glds_k), so results equal the sampled path's bit for bit.
+// Each block also writes its best candidate's controls to part_v / part_b
+// [block][MPC_MAX_STEPS] for the selection's winner re-roll (k_finalize_gen).
+template <int INTEG, int ROT, bool PL2>
+__device__ __forceinline__ void generated_lane(const Consts& K, const double2* s_grid,
+                                               uint32_t n_grid, uint64_t seed, uint64_t g0,
+                                               int n_steps, double (&cst)[2]) {
+  double x[2], y[2], ph[2], sn[2], cs[2];
+  bool bad[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    step_start<ROT>(K, x[j], y[j], ph[j], sn[j], cs[j]);
+    bad[j] = false;
+  }
+  trig::Leads lead = trig::const_leads();
+#pragma unroll 1
+  for (int st = 0; st < n_steps; ++st) {
+    const double2 e0 = s_grid[grid_entry(seed, st, g0, n_grid, 1)];
+    const double2 e1 = s_grid[grid_entry(seed, st, g0 + 1, n_grid, 1)];
+    double ph0 = ROT ? 0.0 : ph[0], ph1 = ROT ? 0.0 : ph[1];
+    step_core<INTEG, ROT, PL2>(x[0], y[0], ph0, sn[0], cs[0], e0.x, e0.y, K, bad[0], &lead);
+    step_core<INTEG, ROT, PL2>(x[1], y[1], ph1, sn[1], cs[1], e1.x, e1.y, K, bad[1], &lead);
+    if (!ROT) {
+      ph[0] = ph0;
+      ph[1] = ph1;
+    }
+  }
+  if constexpr (ROT == kRotCum) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (!bad[j]) cum_pose(K, x[j], y[j], x[j], y[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (bad[j]) {
+      x[j] = K.x;
+      y[j] = K.y;
+      ph[j] = K.phi;
+      for (int sr = 0; sr < n_steps; ++sr) {
+        const double2 e = s_grid[grid_entry(seed, sr, g0 + j, n_grid, 1)];
+        step_safe<INTEG>(x[j], y[j], ph[j], e.x, e.y, K);
+      }
+    }
+    cst[j] = cost(x[j], y[j], K);
+  }
+}
+
+#ifndef MPC_GEN_WAVES
+#define MPC_GEN_WAVES 4   // launch bound of the generated-controls rollout
+#endif
+template <int INTEG, int ROT>
+__global__ __launch_bounds__(kBlock, MPC_GEN_WAVES) void k_rollout_generated(
+    mpc_episode_config_t c, EpisodeState* __restrict__ S, int64_t n_cand, int n_steps,
+    int64_t base, Rec* __restrict__ part, double* __restrict__ part_v,
+    double* __restrict__ part_b) {
+  extern __shared__ double2 s_gen_grid[];   // the expanded grid (dynamic: nv x nb entries)
+  __shared__ double s_v[kEpMaxGrid], s_b[kEpMaxGrid];
+  __shared__ int s_nv, s_nb;
+  if (threadIdx.x < 64) {
+    int nv, nb;
+    episode_grids(c, S->h, s_v, s_b, nv, nb);
+    if (threadIdx.x == 0) {
+      s_nv = nv;
+      s_nb = nb;
+    }
+  }
+  __syncthreads();
+  const int nv = s_nv, nb = s_nb;
+  const uint32_t n_grid = static_cast<uint32_t>(nv) * static_cast<uint32_t>(nb);
+  for (uint32_t k = threadIdx.x; k < n_grid; k += kBlock)
+    s_gen_grid[k] = make_double2(s_v[k / nb], s_b[k % nb]);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {   // as k_episode_sample: the step's grid
+    S->h.nv = nv;
+    S->h.nb = nb;
+    for (int i = 0; i < nv; ++i) S->grid_v[i] = s_v[i];
+    for (int i = 0; i < nb; ++i) S->grid_b[i] = s_b[i];
+  }
+  __syncthreads();
+  const uint64_t seed = S->h.seed;
+  const Consts K = S->h.K;
+  const int64_t n_tiles = (n_cand + kBlock * 2 - 1) / (kBlock * 2);
+  uint64_t best_k = ~0ull;
+  int64_t best_i = INT64_MAX;
+  if (n_grid > 0) {
+    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+      const int64_t c0 = tile * (kBlock * 2) + threadIdx.x * 2;
+      if (c0 < n_cand) {   // n_cand even (host check): the pair is valid
+        double cst[2];
+        const uint64_t g0 = static_cast<uint64_t>(base + c0);
+        if (K.L_pow2)
+          generated_lane<INTEG, ROT, true>(K, s_gen_grid, n_grid, seed, g0, n_steps, cst);
+        else
+          generated_lane<INTEG, ROT, false>(K, s_gen_grid, n_grid, seed, g0, n_steps, cst);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const uint64_t kk = cost_key(cst[j]);
+          if (kk < best_k) {   // ascending index per lane: strict < keeps the first
+            best_k = kk;
+            best_i = c0 + j;
+          }
+        }
+      }
+    }
+  }
+  block_argmin(best_k, best_i);
+  if (threadIdx.x == 0) part[blockIdx.x] = Rec{best_k, best_i};
+  // the block's best candidate's controls, one step per lane
+  __shared__ int64_t s_best;
+  if (threadIdx.x == 0) s_best = best_k == ~0ull ? -1 : best_i;
+  __syncthreads();
+  const int64_t bi = s_best;
+  if (bi >= 0 && threadIdx.x < n_steps) {
+    const double2 e =
+        s_gen_grid[grid_entry(seed, threadIdx.x, static_cast<uint64_t>(base + bi), n_grid, 1)];
+    part_v[blockIdx.x * MPC_MAX_STEPS + threadIdx.x] = e.x;
+    part_b[blockIdx.x * MPC_MAX_STEPS + threadIdx.x] = e.y;
+  }
+}
+
 // _turn_target (math_model_tree.py:142-215 sectors; sign = +1 left, -1 right).
 __device__ inline void turn_target(double ax, double ay, double aphi, double d, double R,
                                    double sign, double& tx, double& ty) {

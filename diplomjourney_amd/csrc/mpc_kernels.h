@@ -731,7 +731,10 @@ __device__ __forceinline__ void load8_rec_sc1(const Rec* const (&p)[8], u64x2 (&
 #ifdef MPC_FIN_TRACE
 __device__ uint64_t g_fin_tick[4];   // debug builds only: stage ticks inside the hook
 #endif
-template <int INTEG, int ROT, bool KDEV, int NT, bool SC1>
+// GEN (generated controls, k_rollout_generated): v / b are [n_part][MPC_MAX_STEPS]
+// — the controls of each rollout block's best candidate — instead of the
+// [n_steps][n_cand] candidate arrays; the winner's are those of its block.
+template <int INTEG, int ROT, bool KDEV, int NT, bool SC1, bool GEN = false>
 __device__ __forceinline__ void finalize_block(
     const Rec* __restrict__ part, int n_part, const Consts& K, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, int64_t index_base,
@@ -808,7 +811,14 @@ __device__ __forceinline__ void finalize_block(
   const uint64_t tr1 = __builtin_amdgcn_s_memrealtime();
 #endif
   Winner w;
-  emit_winner<INTEG, ROT>(K, v, b, n_cand, n_steps, k, i, index_base + i, incumbent, out, &w);
+  if constexpr (GEN) {
+    // (thread 0 holds the winner; emit_winner takes its column from thread 0)
+    // (k_rollout_generated: 2 candidates per lane, tiles dealt round-robin)
+    const int64_t col = k == ~0ull ? 0 : ((i / (kBlock * 2)) % n_part) * MPC_MAX_STEPS;
+    emit_winner<INTEG, ROT>(K, v, b, 1, n_steps, k, col, index_base + i, incumbent, out, &w);
+  } else {
+    emit_winner<INTEG, ROT>(K, v, b, n_cand, n_steps, k, i, index_base + i, incumbent, out, &w);
+  }
 #ifdef MPC_FIN_TRACE
   const uint64_t tr2 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -838,6 +848,19 @@ __device__ __forceinline__ void finalize_block(
     out->traj[30][2] = static_cast<double>(g_fin_tick[2] - g_fin_tick[1]);
   }
 #endif
+}
+
+// The selection of a generated-controls step (GEN finalize_block).
+template <int INTEG, int ROT>
+__global__ __launch_bounds__(kFinBlock) void k_finalize_gen(
+    const Rec* __restrict__ part, int n_part, const Consts* __restrict__ Kdev,
+    const double* __restrict__ part_v, const double* __restrict__ part_b, int n_steps,
+    int64_t index_base, const double* __restrict__ incumbent_dev,
+    mpc_result_t* __restrict__ out, mpc_episode_config_t ecfg, EpisodeHook hook) {
+  const Consts K = *Kdev;
+  finalize_block<INTEG, ROT, true, kFinBlock, false, true>(part, n_part, K, part_v, part_b, 0,
+                                                           n_steps, index_base, *incumbent_dev,
+                                                           out, ecfg, hook);
 }
 
 template <int INTEG, int ROT, bool KDEV>

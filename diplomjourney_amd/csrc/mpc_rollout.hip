@@ -385,6 +385,57 @@ int mpc_episode_sample(const mpc_episode_config_t* cfg, void* state, double* v_s
   return last_hip_status();
 }
 
+// Generated controls: the block records, then [grid][MPC_MAX_STEPS] v and beta
+// of each block's best candidate.
+static int64_t gen_grid(int64_t n_cand) { return rollout_grid<2>(n_cand); }
+static size_t gen_ctl_offset(int64_t n_cand) {
+  return (static_cast<size_t>(gen_grid(n_cand)) * sizeof(Rec) + 255) & ~static_cast<size_t>(255);
+}
+
+size_t mpc_episode_generate_workspace_bytes(int64_t n_cand, int32_t n_steps) {
+  (void)n_steps;
+  if (n_cand < 2) return 0;
+  return gen_ctl_offset(n_cand) +
+         2 * static_cast<size_t>(gen_grid(n_cand)) * MPC_MAX_STEPS * sizeof(double);
+}
+
+int mpc_episode_generate_step(const mpc_episode_config_t* cfg, void* state, int64_t n_cand,
+                              int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
+                              size_t ws_bytes, mpc_result_t* out, mpc_episode_log_t* log,
+                              int32_t log_capacity, mpc_stream_t stream) {
+  if (check_episode_cfg(cfg) != MPC_OK || !state || !out || n_steps < 1 ||
+      n_steps > MPC_MAX_STEPS || index_base < 0 || log_capacity < 0)
+    return MPC_ERR_ARG;
+  if (n_cand < 2 || n_cand % 2 != 0) return MPC_ERR_ARG;   // two candidates per lane
+  if (mode_ok(integrator) != MPC_OK) return MPC_ERR_UNSUPPORTED;
+  if (!ws || ws_bytes < mpc_episode_generate_workspace_bytes(n_cand, n_steps))
+    return MPC_ERR_WORKSPACE;
+  // the expanded grid in LDS: at most (1 + 2 ratio_v) x (1 + 2 ratio_beta) entries
+  static_assert(kEpMaxGrid * kEpMaxGrid * sizeof(double2) <= 64 * 1024, "grid LDS bound");
+  const int64_t nv = std::min<int64_t>(kEpMaxGrid, 1 + 2 * static_cast<int64_t>(cfg->ratio_v));
+  const int64_t nb =
+      std::min<int64_t>(kEpMaxGrid, 1 + 2 * static_cast<int64_t>(cfg->ratio_beta));
+  const size_t lds = static_cast<size_t>(nv * nb) * sizeof(double2);
+  EpisodeState* S = static_cast<EpisodeState*>(state);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  char* w = static_cast<char*>(ws);
+  Rec* part = reinterpret_cast<Rec*>(w);
+  const int64_t grid = gen_grid(n_cand);
+  double* part_v = reinterpret_cast<double*>(w + gen_ctl_offset(n_cand));
+  double* part_b = part_v + grid * MPC_MAX_STEPS;
+  const EpisodeHook hook{&S->h, log, log_capacity, S->chain_pub, kPubWords};
+  dispatch_mode(integrator, [&](auto integ, auto rot) {
+    constexpr int I = decltype(integ)::value;
+    constexpr int R = decltype(rot)::value;
+    k_rollout_generated<I, R><<<grid, kBlock, lds, st>>>(*cfg, S, n_cand, n_steps, index_base,
+                                                         part, part_v, part_b);
+    k_finalize_gen<I, R><<<1, kFinBlock, 0, st>>>(part, static_cast<int>(grid), &S->h.K, part_v,
+                                                  part_b, n_steps, index_base, &S->h.incumbent,
+                                                  out, *cfg, hook);
+  });
+  return last_hip_status();
+}
+
 int mpc_episode_partials(void* state, const double* v_sc, const double* beta_sc, int64_t n_cand,
                          int32_t n_steps, int32_t integrator, void* ws, size_t ws_bytes,
                          mpc_stream_t stream) {

@@ -178,7 +178,8 @@ class DeviceEpisode:
 
     def __init__(self, engine, n_cand_total, n_steps, rank=0, world=1, seed=20261015,
                  integrator="rect", group=None, start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3),
-                 log_capacity=4096, split=True, exchange=None, chain=False, L=None):
+                 log_capacity=4096, split=True, exchange=None, chain=False, L=None,
+                 generate=False):
         self.eng = engine
         self.lib = native.lib()
         self.n_total = int(n_cand_total)
@@ -216,6 +217,13 @@ class DeviceEpisode:
         # flush() completes the last one.
         self.chain = bool(chain)
         self._ws = [self.ws, torch.empty_like(self.ws)] if self.chain else [self.ws]
+        # generate: steps without caller controls draw their candidates inside
+        # the rollout (mpc_episode_generate_step) instead of sampling them into
+        # v_sc / b_sc first — the same candidates, never written to HBM
+        self.generate = bool(generate)
+        if self.generate and self.exchange:
+            raise ValueError("generated controls: one GPU (no exchange step)")
+        self._gen_ws = None
         self._pending = None
         self._epoch = 0
         self._checked = {}
@@ -325,6 +333,23 @@ class DeviceEpisode:
         st = self._stream()
         L = self.lib
         self.flush()
+        if controls is None and self.generate:
+            if self.exchange:
+                raise ValueError("generated controls: one GPU (no exchange step)")
+            if self._gen_ws is None:
+                self._gen_ws = torch.empty(self.lib.mpc_episode_generate_workspace_bytes(
+                    self.n_local, self.n_steps), dtype=torch.uint8, device=self.state.device)
+            if events:
+                events[0].record()
+            native.check(L.mpc_episode_generate_step(
+                ctypes.byref(self.cfg), self.state.data_ptr(), self.n_local, self.n_steps,
+                self.lo, self._integ, self._gen_ws.data_ptr(), self._gen_ws.numel(),
+                self.local.data_ptr(), self.log.data_ptr(), self.log_capacity, st),
+                "mpc_episode_generate_step")
+            if events:
+                events[1].record()
+            self.steps_enqueued += 1
+            return
         if controls is None:
             native.check(L.mpc_episode_sample(ctypes.byref(self.cfg), self.state.data_ptr(),
                                               self.v_sc.data_ptr(), self.b_sc.data_ptr(),

@@ -261,6 +261,20 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
                            const double* beta_prev, mpc_result_t* out_prev,
                            const mpc_result_t* gathered, int32_t n_gathered,
                            mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
+/* Generated controls (one GPU): one MPC step of the device-resident episode
+ * whose candidates are never materialised — the same candidates, bit for bit,
+ * as mpc_episode_sample followed by mpc_episode_step (advance = cfg) on the
+ * sampler's arrays: every block builds the step's grid (math_model_tree.py
+ * :239-256, slow-down :312-316) in LDS and draws each candidate-step's entry
+ * with the sampler's hash (constant prefix included), rolls it out, and the
+ * selection re-rolls the winner and advances the episode.  n_cand even;
+ * ws: mpc_episode_generate_workspace_bytes(n_cand, n_steps).  The grid (at
+ * most 64 x 64 entries) is staged in LDS. */
+size_t mpc_episode_generate_workspace_bytes(int64_t n_cand, int32_t n_steps);
+int mpc_episode_generate_step(const mpc_episode_config_t* cfg, void* state, int64_t n_cand,
+                              int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
+                              size_t ws_bytes, mpc_result_t* out, mpc_episode_log_t* log,
+                              int32_t log_capacity, mpc_stream_t stream);
 /* Persistent run (integrator MPC_INTEG_RECT | MPC_HEADING_CUMULATIVE, one GPU):
  * k_steps MPC steps of the device-resident episode in ONE launch — the same
  * steps as k_steps two-launch mpc_episode_step calls (advance non-NULL) on the

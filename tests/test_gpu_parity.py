@@ -684,3 +684,55 @@ def test_bench_contract(extra):
         assert rf["kernel"] == "k_episode_chain"
         assert d["config"]["step_launches"].startswith("chained")
     assert rf["traffic"] is not None and abs(rf["traffic"] / 160e6 - 1) < 0.01
+
+
+@pytest.mark.parametrize("integ,n,L", [("rect+cum", 100_000, None), ("rect+rot", 100_000, None),
+                                       ("qk21", 20_000, None), ("rect+cum", 1_100_000, 0.45)])
+def test_generated_episode_matches_sampled(engine, integ, n, L):
+    """Generated controls (mpc_episode_generate_step: grid + sampler fused into
+    the rollout, candidates never in HBM) log exactly the steps of the sampled
+    episode (mpc_episode_sample -> arrays -> rollout -> selection) over 150
+    steps with the operator events and an episode restart, for the default
+    integrators, a non-power-of-two wheelbase and several tiles per block; the
+    final winner record (re-rolled trajectory included) is identical too."""
+    from diplomjourney_amd.episode import DeviceEpisode
+    ns, steps = 10, 150
+    logs, outs = [], []
+    for gen in (False, True):
+        ep = DeviceEpisode(engine, n, ns, integrator=integ, log_capacity=256, L=L, generate=gen)
+        ep.cfg.max_steps = 120            # forces an episode restart inside the run
+        ep.reset()
+        for _ in range(steps):
+            ep.step()
+        logs.append([bytes(r) for r in ep.read_log()])
+        outs.append(ep.local.cpu().numpy().tobytes())
+    assert len(logs[0]) == steps
+    assert logs[1] == logs[0]
+    assert outs[1] == outs[0]
+
+
+def test_generated_step_arguments(engine):
+    """mpc_episode_generate_step rejects odd candidate counts and a short
+    workspace before launching; the largest grid (64 x 64 entries, 64 KiB of
+    LDS) launches."""
+    import ctypes
+    from diplomjourney_amd import abi, native
+    from diplomjourney_amd.episode import DeviceEpisode
+    L = native.lib()
+    ep = DeviceEpisode(engine, 1000, 10, integrator="rect+cum", generate=True)
+    ep.step()                             # allocates the workspace
+    wsb = L.mpc_episode_generate_workspace_bytes(1000, 10)
+    assert wsb >= 16 and L.mpc_episode_generate_workspace_bytes(1, 10) == 0
+
+    def call(n=1000, wsb=wsb, ratio=None):
+        cfg = ep.cfg
+        if ratio is not None:
+            cfg = type(ep.cfg).from_buffer_copy(ep.cfg)
+            cfg.ratio_v = cfg.ratio_beta = ratio
+        return L.mpc_episode_generate_step(ctypes.byref(cfg), ep.state.data_ptr(), n, 10, 0,
+                                           ep._integ, ep._gen_ws.data_ptr(), wsb,
+                                           ep.local.data_ptr(), ep.log.data_ptr(), 16, None)
+
+    assert call(n=999) == abi.MPC_ERR_ARG
+    assert call(wsb=wsb - 1) == abi.MPC_ERR_WORKSPACE
+    assert call(ratio=100.0) == abi.MPC_OK
