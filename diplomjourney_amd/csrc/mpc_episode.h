@@ -235,7 +235,9 @@ __device__ __forceinline__ void generated_lane(const Consts& K, const double2* s
 #ifndef MPC_GEN_WAVES
 #define MPC_GEN_WAVES 4   // launch bound of the generated-controls rollout
 #endif
-template <int INTEG, int ROT>
+// PL2 (wheelbase a power of two) is a template parameter picked by the host
+// from cfg, as in the chained step (one rollout variant per kernel).
+template <int INTEG, int ROT, bool PL2>
 __global__ __launch_bounds__(kBlock, MPC_GEN_WAVES) void k_rollout_generated(
     mpc_episode_config_t c, EpisodeState* __restrict__ S, int64_t n_cand, int n_steps,
     int64_t base, Rec* __restrict__ part, double* __restrict__ part_v,
@@ -257,6 +259,8 @@ __global__ __launch_bounds__(kBlock, MPC_GEN_WAVES) void k_rollout_generated(
   for (uint32_t k = threadIdx.x; k < n_grid; k += kBlock)
     s_gen_grid[k] = make_double2(s_v[k / nb], s_b[k % nb]);
   if (blockIdx.x == 0 && threadIdx.x == 0) {   // as k_episode_sample: the step's grid
+    // a state reset with another wheelbase form than cfg's: flag it (chain error 2)
+    if ((S->h.K.L_pow2 != 0) != PL2) S->chain_error = 2u;
     S->h.nv = nv;
     S->h.nb = nb;
     for (int i = 0; i < nv; ++i) S->grid_v[i] = s_v[i];
@@ -274,10 +278,7 @@ __global__ __launch_bounds__(kBlock, MPC_GEN_WAVES) void k_rollout_generated(
       if (c0 < n_cand) {   // n_cand even (host check): the pair is valid
         double cst[2];
         const uint64_t g0 = static_cast<uint64_t>(base + c0);
-        if (K.L_pow2)
-          generated_lane<INTEG, ROT, true>(K, s_gen_grid, n_grid, seed, g0, n_steps, cst);
-        else
-          generated_lane<INTEG, ROT, false>(K, s_gen_grid, n_grid, seed, g0, n_steps, cst);
+        generated_lane<INTEG, ROT, PL2>(K, s_gen_grid, n_grid, seed, g0, n_steps, cst);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const uint64_t kk = cost_key(cst[j]);

@@ -424,11 +424,17 @@ int mpc_episode_generate_step(const mpc_episode_config_t* cfg, void* state, int6
   double* part_v = reinterpret_cast<double*>(w + gen_ctl_offset(n_cand));
   double* part_b = part_v + grid * MPC_MAX_STEPS;
   const EpisodeHook hook{&S->h, log, log_capacity, S->chain_pub, kPubWords};
+  int e;
+  const bool pl2 = frexp(cfg->L, &e) == 0.5;   // as consts_from_problem decides
   dispatch_mode(integrator, [&](auto integ, auto rot) {
     constexpr int I = decltype(integ)::value;
     constexpr int R = decltype(rot)::value;
-    k_rollout_generated<I, R><<<grid, kBlock, lds, st>>>(*cfg, S, n_cand, n_steps, index_base,
-                                                         part, part_v, part_b);
+    if (pl2)
+      k_rollout_generated<I, R, true><<<grid, kBlock, lds, st>>>(*cfg, S, n_cand, n_steps,
+                                                                 index_base, part, part_v, part_b);
+    else
+      k_rollout_generated<I, R, false><<<grid, kBlock, lds, st>>>(*cfg, S, n_cand, n_steps,
+                                                                  index_base, part, part_v, part_b);
     k_finalize_gen<I, R><<<1, kFinBlock, 0, st>>>(part, static_cast<int>(grid), &S->h.K, part_v,
                                                   part_b, n_steps, index_base, &S->h.incumbent,
                                                   out, *cfg, hook);
