@@ -36,7 +36,8 @@ Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the
 chained k_episode_chain by default, k_rollout_argmin_stream for two-launch
 steps): algorithmic bytes 16 B per candidate-step (fp64 v and beta read once)
 / its average duration, from HIP events around 100 back-to-back launches on
-the episode's stream and controls.
+the episode's stream and controls; with chained steps `roofline_rollout_only`
+adds the same controls through the rollout kernel alone.
 `cpu_baseline` is the reference-structured Python port (scipy quad) on this
 host's cores, rank 0 at N=1 only, on a bounded sample of the same candidates;
 it runs before the GPU is initialised (it forks worker processes).
@@ -233,6 +234,7 @@ def main():
                            generate=inputs == "generated")
     pool = make_pool(eng, ep, n_steps, args.steps) if inputs == "resident" else None
     persistent = args.run
+    rollout_ms = None
     # the launch that carries the step: the chained kernel (rollout of step k +
     # completion of step k-1), the persistent run, or the rollout kernel
     chained = (not persistent and not exchange and getattr(ep, "chain", False)
@@ -252,6 +254,9 @@ def main():
         kern_ms = main_run["kernel_in_step_ms"]
         if chained:
             kern_ms = chain_pass(ep, pool)
+            # for comparison: the same controls through the rollout kernel alone
+            # (the chained launch adds block 0's completion of the previous step)
+            rollout_ms = kernel_pass(ep, pool)
         elif inputs == "generated":
             pass   # events around the generated rollout + selection (no HBM roofline)
         elif hasattr(ep, "partials"):
@@ -323,6 +328,9 @@ def main():
         "kernel_ms": kern_ms, "kernel_in_step_ms": main_run["kernel_in_step_ms"],
         "roofline": (None if inputs == "generated" else
                      roofline(achieved, bytes_launch, args.traffic_json, kernel=kernel)),
+        "roofline_rollout_only": (None if rollout_ms is None else
+                                  roofline(bytes_launch / (rollout_ms * 1e-3) / 1e9, bytes_launch,
+                                           None, kernel="k_rollout_argmin_stream")),
         "other_inputs": other,
         "generated_inputs": generated,
         "cpu_baseline": cpu,

@@ -683,6 +683,8 @@ def test_bench_contract(extra):
         assert d["config"]["integrator"] == "rect+cum"
         assert rf["kernel"] == "k_episode_chain"
         assert d["config"]["step_launches"].startswith("chained")
+        ro = d["roofline_rollout_only"]
+        assert ro["kernel"] == "k_rollout_argmin_stream" and 0 < ro["frac"] < 1
     assert rf["traffic"] is not None and abs(rf["traffic"] / 160e6 - 1) < 0.01
 
 
