@@ -134,3 +134,29 @@ def test_candidate_enumeration_order():
     assert v_sc.shape == (3, 6)
     assert v_sc[0].tolist() == [0.1, 0.1, 0.1, 0.2, 0.2, 0.2]
     assert b_sc[2].tolist() == [-1.0, 0.0, 1.0, -1.0, 0.0, 1.0]
+
+
+def test_bench_defaults(monkeypatch):
+    """bench.py's defaults: config C on one GPU, the chained rect+cum step for
+    the episode workloads (B, C, D), rect+rot for E/F/G, 500 timed steps for
+    the ~40-us workloads; the persistent run needs rect+cum."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    def parse(*argv):
+        monkeypatch.setattr(sys, "argv", ["bench.py", *argv])
+        return bench.parse()
+
+    a = parse()
+    assert (a.workload, a.gpus, a.steps, a.warmup, a.integrator, a.inputs) == (
+        "C", 1, 500, 20, "rect+cum", "resident")
+    assert not a.no_chain and not a.run
+    assert parse("--workload", "D").integrator == "rect+cum"
+    assert parse("--workload", "B").integrator == "rect+cum"
+    assert parse("--workload", "E").integrator == "rect+rot"
+    f = parse("--workload", "F")
+    assert (f.integrator, f.steps) == ("rect+rot", 50)
+    assert parse("--integrator", "qk21").integrator == "qk21"
+    assert parse("--inputs", "generated").inputs == "generated"
