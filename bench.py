@@ -386,6 +386,11 @@ def run_steps(args, ep, pool, use_graph, world, device):
     flush = getattr(ep, "flush", lambda: None)   # completes a chained step left pending
     for i in range(args.warmup):
         step(i)
+    # (untimed) until ~10 ms of steps have run: the GPU's clocks ramp over the
+    # first few hundred launches (38 -> 34 us per chained step), which a short
+    # --warmup leaves in the latency pass's p50
+    for i in range(max(0, 300 - args.warmup)):
+        step(i)
     flush()
     Ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     # latency pass: one event per step start (more events per step would add
