@@ -116,6 +116,10 @@ __device__ __forceinline__ void ft_leaves_body(const Consts& K, double atan_t,
     const int64_t k2_lo = c * kFtChunk;
     const int64_t k2_hi = k2_lo + kFtChunk < s1 ? k2_lo + kFtChunk : s1;
     const int64_t j0 = mm * s1;
+#ifndef MPC_FT_UNROLL
+#define MPC_FT_UNROLL 4   // k2 iterations interleaved (A/B: 1 -> 2 -> 4 = 353 -> 337 -> 335 us per config-F step)
+#endif
+#pragma unroll MPC_FT_UNROLL
     for (int64_t k2 = k2_lo; k2 < k2_hi; ++k2) {   // wave-uniform control
       const FtCtl u = ctl[k2];
       const FtState lf = ft_apply<INTEG, ROT>(l1, u, K);
