@@ -738,3 +738,28 @@ def test_generated_step_arguments(engine):
     assert call(n=999) == abi.MPC_ERR_ARG
     assert call(wsb=wsb - 1) == abi.MPC_ERR_WORKSPACE
     assert call(ratio=100.0) == abi.MPC_OK
+
+
+@pytest.mark.parametrize("ns", [2, 3, 12])
+def test_short_and_long_horizons_chain_and_run(engine, ns):
+    """Horizons around the head prefetch three steps before a loop's end
+    (none for N = 2, at the first step for N = 3) and the config-D length
+    N = 12: the chained steps and the persistent run log exactly the
+    two-launch rect+cum episode over 60 steps with a restart."""
+    from diplomjourney_amd.episode import DeviceEpisode
+    n, steps = 20_000, 60
+    pool = _pool(engine, n, ns, 4, 900 + ns)
+    batches = [pool[i % 4] for i in range(steps)]
+    _, want = _two_launch_log(engine, n, ns, batches, max_steps=40)
+    assert len({r[9] for r in want}) >= 2, "no episode restart exercised"
+    ch = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=512, chain=True)
+    ch.cfg.max_steps = 40
+    for c in batches:
+        ch.step(controls=c)
+    ch.flush()
+    assert _episode_log(ch) == want
+    run = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=512)
+    run.cfg.max_steps = 40
+    run.run(batches)
+    assert _episode_log(run) == want
+    assert run.chain_error() == 0 and ch.chain_error() == 0
