@@ -641,8 +641,11 @@ def bench_robots(args, wl, eng, rank, world, cpu):
                    "candidates_per_robot": cand, "integrator": args.integrator,
                    "parallelism": f"robot-sharded x{world}, no exchange"},
         "p50_ms": percentile(step_ms, 50), "kernel_ms": kern_ms,
+        # kern_ms brackets both launches of the call (the rollout and the
+        # per-robot finalize, ~7 us of it)
         "roofline": roofline(bytes_launch / (kern_ms * 1e-3) / 1e9, bytes_launch,
-                             args.traffic_json),
+                             args.traffic_json,
+                             kernel="k_rollout_argmin_batched+k_finalize_batched"),
         "cpu_baseline": cpu,
     }
     if rank == 0:

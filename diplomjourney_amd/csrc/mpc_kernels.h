@@ -957,13 +957,52 @@ __device__ __forceinline__ Consts consts_from_problem(const mpc_problem_t& p) {
   return K;
 }
 
+// Block-uniform constants computed on the VALU (consts_from_problem) moved to
+// SGPRs: hipcc keeps VALU results in VGPRs even when every lane holds the same
+// value, which costs the batched kernel its fifth wave (120 VGPRs -> spills).
+__device__ __forceinline__ double uniform_d(double a) {
+  const uint64_t u = static_cast<uint64_t>(__double_as_longlong(a));
+  const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(u)));
+  const uint64_t hi =
+      static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(u >> 32)));
+  return __longlong_as_double(static_cast<long long>((hi << 32) | lo));
+}
+
+__device__ __forceinline__ Consts uniform_consts(const Consts& k) {
+  Consts K;
+  K.x = uniform_d(k.x);
+  K.y = uniform_d(k.y);
+  K.phi = uniform_d(k.phi);
+  K.x_t = uniform_d(k.x_t);
+  K.y_t = uniform_d(k.y_t);
+  K.x_0 = uniform_d(k.x_0);
+  K.y_0 = uniform_d(k.y_0);
+  K.A = uniform_d(k.A);
+  K.B = uniform_d(k.B);
+  K.C1 = uniform_d(k.C1);
+  K.C2 = uniform_d(k.C2);
+  K.den = uniform_d(k.den);
+  K.L = uniform_d(k.L);
+  K.inv_L = uniform_d(k.inv_L);
+  K.h = uniform_d(k.h);
+  K.hlgth = uniform_d(k.hlgth);
+  K.s0 = uniform_d(k.s0);
+  K.c0 = uniform_d(k.c0);
+  K.L_pow2 = __builtin_amdgcn_readfirstlane(k.L_pow2);
+  K.pad_ = 0;
+  return K;
+}
+
 // --------------------------- batched robots --------------------------------
+// The wide variant runs the streaming kernel's lane (LDS-DMA ring): the same
+// 5 waves per SIMD (4 at the default bound: 120 VGPRs).
 template <int CPL, int INTEG, int ROT>
-__global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin_batched(
+__global__ __launch_bounds__(kBlock, CPL == kCplWide ? MPC_STREAM_WAVES : MPC_MIN_WAVES) void
+k_rollout_argmin_batched(
     const mpc_problem_t* __restrict__ probs, const double* __restrict__ v,
     const double* __restrict__ b, int64_t cand, int n_steps, int64_t ld, Rec* __restrict__ part) {
   const int r = blockIdx.y;
-  const Consts K = consts_from_problem(probs[r]);
+  const Consts K = uniform_consts(consts_from_problem(probs[r]));
   uint64_t best_k = ~0ull;
   int64_t best_i = INT64_MAX;
   const int64_t tiles = (cand + kBlock * CPL - 1) / (kBlock * CPL);
