@@ -259,6 +259,64 @@ def test_batched_robots_vs_oracle(engine, oracle):
             _close_traj(g, o, ns)
 
 
+def test_full_size_config_e_batched(engine, oracle):
+    """Config E at its full size, built as bench.py builds it (1024 robots x
+    1e4 candidates, N=8, per-robot PCG64 problems and sampler seeds), in the
+    bench's rect+rot mode: every robot's winner equals the host replica of the
+    kernel's arithmetic, its cost and trajectory to within ulps; and for a
+    sample of robots the oracle (reference arithmetic, rect) picks the same
+    candidate.  (Not bitwise: the batched kernel derives each robot's
+    constants on the device — sin/cos of the start heading with the kernel's
+    own sincos, squares as x*x — where the replica, like the single-problem
+    host path, takes libm's; robot 527's winner, for one, lands 1 ulp apart
+    in one coordinate.)"""
+    from harness import replica_rollout
+    from diplomjourney_amd.abi import make_problem
+    from diplomjourney_amd.expansion import problems_to_device, results_from_device
+    R, cand, ns = 1024, 10_000, 8
+    probs = []
+    for r in range(R):
+        g = np.random.default_rng(20261015 + r)
+        x0, y0 = g.uniform(-10, 10, 2)
+        phi0 = g.uniform(-math.pi, math.pi)
+        xt, yt = g.uniform(x0 - 10, x0 + 10), g.uniform(y0 - 10, y0 + 10)
+        probs.append(make_problem(x0, y0, phi0, xt, yt, x0, y0, 0.5, 0.05, 0.1))
+    V, B = _grid451()
+    v = torch.empty((ns, R * cand), dtype=torch.float64, device="cuda")
+    b = torch.empty_like(v)
+    for r in range(R):
+        engine.sample_controls(_dev(V), _dev(B), cand, ns, 20261015 + r,
+                               v_out=v[:, r * cand:], beta_out=b[:, r * cand:], ld=R * cand)
+    out = engine.rollout_argmin_batched(problems_to_device(probs, "cuda"), v, b, cand,
+                                        integrator="rect+rot")
+    got = results_from_device(out)
+    vh, bh = v.cpu().numpy(), b.cpu().numpy()
+    exact = 0
+    for r in range(R):
+        cols = slice(r * cand, (r + 1) * cand)
+        st, costs = replica_rollout(probs[r], vh[:, cols], bh[:, cols], "rect+rot")
+        k = int(np.argmin(costs))
+        g = got[r]
+        if g.index != k:     # only a near-tie below the constants' ulp noise
+            assert abs(costs[g.index] - costs[k]) <= 1e-13 * abs(costs[k]), r
+            continue
+        assert math.isclose(g.cost, costs[k], rel_tol=1e-14), r
+        d = np.abs(np.array(g.trajectory()) - st[:, :, k]).max()
+        assert d <= 1e-13, (r, d)
+        exact += g.trajectory() == [list(st[s, :, k]) for s in range(ns)]
+    assert exact >= R // 2       # most winners still bit-identical to the replica
+    sample = list(range(0, R, 64))
+    ref = oracle.rollout_argmin_batched([probs[r] for r in sample],
+                                        np.concatenate([vh[:, r * cand:(r + 1) * cand]
+                                                        for r in sample], axis=1),
+                                        np.concatenate([bh[:, r * cand:(r + 1) * cand]
+                                                        for r in sample], axis=1),
+                                        cand, integ="rect")
+    for r, o in zip(sample, ref):
+        assert got[r].index == o.index, r
+        _close_traj(got[r], o, ns)
+
+
 def test_states_out_vs_oracle(engine, oracle):
     from diplomjourney_amd.abi import make_problem
     n, ns = 5003, 6
