@@ -92,6 +92,30 @@ def test_gpu_bitwise_equals_replica(engine, n, ns, integ):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("integ", ["rect", "rect+rot"])
+def test_gpu_trig_bitwise_equals_host_build(engine, integ):
+    """The device build of mpc_trig.h (hardware reciprocal estimate in
+    tan_small, device rint/fma) against its host build, through the
+    production kernel: every state of 2e6 candidates with uniformly random
+    steering angles over the whole regular range |beta| <= 1.1 (not just the
+    reference grid's 41 values) and random speeds, from a random start
+    heading — bit for bit."""
+    from diplomjourney_amd.abi import make_problem
+    rng = np.random.default_rng(29)
+    n, ns = 2_000_000, 2
+    v = rng.uniform(0.0, 1.0, (ns, n))
+    b = rng.uniform(-1.1, 1.1, (ns, n))
+    p = make_problem(0.3, -0.7, rng.uniform(-3, 3), 2, 3, 0, 0, 0.5, 0.05, 0.1)
+    st, costs = replica_rollout(p, v, b, integ)
+    states = torch.empty((ns, 3, n), dtype=torch.float64, device="cuda")
+    engine.rollout_argmin(p, torch.as_tensor(v, device="cuda"), torch.as_tensor(b, device="cuda"),
+                          incumbent=INC_MAX, integrator=integ, states=states)
+    got = states.cpu().numpy()
+    assert np.array_equal(got, st), int((got != st).sum())
+    assert engine.fetch().cost == costs.min()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("integ", ["rect+rot", "rect", "qk21", "qk21+rot", "rect+cum"])
 def test_gpu_irregular_candidates_stream_kernel(engine, integ):
     """Irregular candidates (|beta| > 1.1 at some step; in rotation mode also
