@@ -38,9 +38,6 @@ struct EpisodeState {
   // the launch's epoch ((dword << 32) | epoch), so one coherent load per word
   // says whether its value is this step's.  Tag 0: none.
   alignas(128) uint64_t chain_pub[kPubWords];
-  // Tile claims of a chained launch: (epoch << 32) | tiles claimed so far,
-  // reset by the launch's block 0 (k_episode_chain).
-  alignas(128) uint64_t chain_claim;
 };
 
 __device__ inline Consts episode_consts(const EpisodeHead& S, double x, double y, double phi,
@@ -105,7 +102,6 @@ __global__ void k_episode_reset(mpc_episode_config_t c, EpisodeState* __restrict
   S->done = 0u;
   S->chain_error = 0u;
   for (int q = 0; q < kPubWords; ++q) S->chain_pub[q] = 0ull;
-  S->chain_claim = 0ull;
 }
 
 // Grids (:239-256) with the reference's expressions and the slow-down
@@ -606,13 +602,6 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
   }
 #endif
   if (blockIdx.x == 0) {
-#if MPC_CHAIN_CLAIM
-    // this launch's tile claims start at 0 (tagged: a claim that meets the
-    // previous launch's word waits for this store, see claim_next)
-    if (threadIdx.x == 0)
-      __hip_atomic_store(&S->chain_claim, static_cast<uint64_t>(epoch) << 32, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-#endif
     if (has_prev) {
       if constexpr (MODE == kChainFin) {
         const Consts Kp = S->h.K;
@@ -676,15 +665,7 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
   // the last control loads, so the end of the loop normally finds them there.
   uint64_t w_pre = 0;
   bool pre_issued = false;
-#if MPC_CHAIN_CLAIM
-  uint64_t claim_old = 0;   // thread 0: the claim issued with this tile's last loads
-#endif
   auto mid = [&]() {
-#if MPC_CHAIN_CLAIM
-    if (threadIdx.x == 0)
-      claim_old = __hip_atomic_fetch_add(&S->chain_claim, 1ull, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-#endif
     if (waited || pre_issued || s_final) return;
     pre_issued = true;
     if (threadIdx.x < kPubWords)
@@ -719,116 +700,6 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
   const int64_t n_tiles = (n_cand + kBlock * CPL - 1) / (kBlock * CPL);
   uint64_t best_k = ~0ull;
   int64_t best_i = INT64_MAX;
-#if MPC_CHAIN_CLAIM
-  // One resident round of blocks (the host sizes the grid): block b rolls out
-  // tile b - 1, then claims further tiles from a per-launch counter — the
-  // claim is issued with the tile's last control loads (mid) and read after
-  // the loop — so blocks on a faster XCD take more of the second round
-  // instead of each XCD draining its own static eighth of it.
-  {
-    __shared__ int64_t s_next;
-    const int64_t G1 = gridDim.x - 1;
-    int64_t tile = blockIdx.x - 1;
-    while (tile < n_tiles) {
-      const int64_t c0 = tile * (kBlock * CPL) + threadIdx.x * CPL;
-      const int64_t cl = c0 < n_cand ? c0 : n_cand - CPL;
-      double cst[CPL];
-      rollout_lane_glds_k<INTEG, ROT, PL2, decltype(wait), decltype(pre0), decltype(mid),
-                          MPC_CHAIN_PIN>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0, mid);
-      Kl = K;
-      if (c0 < n_cand) {
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) {
-          const uint64_t kk = cost_key(cst[j]);
-          if (rec_less(kk, c0 + j, best_k, best_i)) {
-            best_k = kk;
-            best_i = c0 + j;
-          }
-        }
-      }
-      if (threadIdx.x == 0) {
-        if (n_steps < 3)   // (no mid() call: claim now)
-          claim_old = __hip_atomic_fetch_add(&S->chain_claim, 1ull, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-        uint64_t w = claim_old;
-        uint32_t it = 0;
-        // a claim that met the previous launch's word (block 0 not yet at
-        // its reset) counts nothing: wait for the reset, claim again
-        while (static_cast<uint32_t>(w >> 32) != epoch && ++it < kChainSpinLimit) {
-          __builtin_amdgcn_s_sleep(8);
-          if (static_cast<uint32_t>(__hip_atomic_load(&S->chain_claim, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT) >> 32) == epoch)
-            w = __hip_atomic_fetch_add(&S->chain_claim, 1ull, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (static_cast<uint32_t>(w >> 32) != epoch) {
-          S->chain_error = 1u;
-          s_next = n_tiles;
-        } else {
-          s_next = G1 + static_cast<int64_t>(static_cast<uint32_t>(w));
-        }
-      }
-      __syncthreads();
-      tile = s_next;
-      __syncthreads();   // s_next is rewritten by the next tile
-    }
-  }
-  block_argmin(best_k, best_i);
-  if (threadIdx.x == 0) {
-    part[blockIdx.x - 1] = Rec{best_k, best_i};
-    const int64_t n_rec = n_tiles < kMaxBlocks ? n_tiles : kMaxBlocks;
-    for (int64_t s = blockIdx.x - 1 + (gridDim.x - 1); s < n_rec; s += gridDim.x - 1)
-      part[s] = Rec{~0ull, INT64_MAX};
-  }
-  MPC_TL(4);
-  return;
-#endif
-#if MPC_CHAIN_EVEN
-  // One resident round: every wave of the grid takes an equal contiguous run
-  // of candidate pairs (97-98 at config C), in passes of 64 pairs, so that
-  // all waves end together instead of a second, partial round of tiles
-  // trailing the first.  Lanes past the wave's run roll its last pair again
-  // (result ignored); the pass count is the same for every wave (barriers).
-  {
-    const int lane = threadIdx.x & 63;
-    const int64_t P = n_cand / CPL;
-    const int64_t W = static_cast<int64_t>(gridDim.x - 1) * (kBlock / 64);
-    const int64_t gw = static_cast<int64_t>(blockIdx.x - 1) * (kBlock / 64) + (threadIdx.x >> 6);
-    const int64_t lo = gw * P / W, hi = (gw + 1) * P / W;
-    const int64_t passes = ((P + W - 1) / W + 63) / 64;
-    for (int64_t pass = 0; pass < passes; ++pass) {
-      const int64_t pair = lo + pass * 64 + lane;
-      const bool valid = pair < hi;
-      const int64_t c0 = CPL * (valid ? pair : (hi > lo ? hi - 1 : 0));
-      double cst[CPL];
-      rollout_lane_glds_k<INTEG, ROT, PL2, decltype(wait), decltype(pre0), decltype(mid),
-                          MPC_CHAIN_PIN>(K, Kl, v, b, n_cand, c0, n_steps, cst, wait, pre0, mid);
-      Kl = K;
-      if (valid) {
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) {
-          const uint64_t kk = cost_key(cst[j]);
-          if (kk < best_k) {
-            best_k = kk;
-            best_i = c0 + j;
-          }
-        }
-      }
-    }
-  }
-  block_argmin(best_k, best_i);
-  if (threadIdx.x == 0) {
-    part[blockIdx.x - 1] = Rec{best_k, best_i};
-    // the consumers reduce the records of a tile-per-block grid: the slots
-    // this shorter grid does not own hold the empty record
-    const int64_t n_rec = n_tiles < kMaxBlocks ? n_tiles : kMaxBlocks;
-    for (int64_t s = blockIdx.x - 1 + (gridDim.x - 1); s < n_rec; s += gridDim.x - 1)
-      part[s] = Rec{~0ull, INT64_MAX};
-  }
-  MPC_TL(4);
-  (void)n_tiles;
-  return;
-#endif
   for (int64_t tile = blockIdx.x - 1; tile < n_tiles; tile += gridDim.x - 1) {
     const int64_t c0 = tile * (kBlock * CPL) + threadIdx.x * CPL;
     // lanes past the end of a partial tile roll the last pair again (result

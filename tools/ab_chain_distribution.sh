@@ -1,7 +1,10 @@
 #!/bin/bash
 # A/B of chained-kernel work distributions (round 2): tile per block (base),
-# equal per-wave runs (even), dynamic tile claims (claim), each built with
+# equal per-wave runs (even: -DMPC_CHAIN_EVEN=1), dynamic tile claims (claim:
+# -DMPC_CHAIN_CLAIM=1, with -DMPC_CHAIN_TIMELINE for tlclaim), each built with
 # tools/build_variant.sh; then the claim variant's timeline and chain tests.
+# The even / claim code paths were removed after this A/B (both slower); they
+# are in commit 48e9dbb.
 set -o pipefail
 mkdir -p gpurun_out/s3
 O=gpurun_out/s3/ab_claim.txt
