@@ -10,12 +10,12 @@ mkdir -p gpurun_out/s3
 O=gpurun_out/s3/ab_claim.txt
 : > $O
 for r in 1 2; do
-  for var in ${VARS:-base claim}; do
+  for var in ${VARS:-base xclaim}; do
     DIPLOMJOURNEY_MPC_LIB=tools/var_$var.so timeout -k 10 120 python tools/time_chain.py >> $O 2>&1 || exit 1
   done
 done
-DIPLOMJOURNEY_MPC_LIB=tools/var_tlclaim.so timeout -k 10 120 python tools/chain_timeline.py > gpurun_out/s3/timeline_claim.txt 2>&1 || exit 1
-DIPLOMJOURNEY_MPC_LIB=tools/var_claim.so timeout -k 10 400 python -u -m pytest tests -x -q -m gpu -k "chain or short_and_long" --timeout 120 --timeout-method thread > gpurun_out/s3/pytest_claim.log 2>&1
+DIPLOMJOURNEY_MPC_LIB=tools/var_tl${TLV:-xclaim}.so timeout -k 10 120 python tools/chain_timeline.py > gpurun_out/s3/timeline_claim.txt 2>&1 || exit 1
+DIPLOMJOURNEY_MPC_LIB=tools/var_${TV:-xclaim}.so timeout -k 10 400 python -u -m pytest tests -x -q -m gpu -k "chain or short_and_long" --timeout 120 --timeout-method thread > gpurun_out/s3/pytest_claim.log 2>&1
 rc=$?
 grep "chained launch" $O; tail -3 gpurun_out/s3/pytest_claim.log; head -16 gpurun_out/s3/timeline_claim.txt
 exit $rc
