@@ -38,11 +38,6 @@ struct EpisodeState {
   // the launch's epoch ((dword << 32) | epoch), so one coherent load per word
   // says whether its value is this step's.  Tag 0: none.
   alignas(128) uint64_t chain_pub[kPubWords];
-#if MPC_CHAIN_XCLAIM
-  // Second-round tile claims of a chained launch, one pool per XCD (own
-  // 128-B line each): (epoch << 32) | claims so far, reset by block 0.
-  alignas(128) uint64_t chain_claim[8][16];
-#endif
 };
 
 __device__ inline Consts episode_consts(const EpisodeHead& S, double x, double y, double phi,
@@ -607,11 +602,6 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
   }
 #endif
   if (blockIdx.x == 0) {
-#if MPC_CHAIN_XCLAIM
-    if (threadIdx.x < 8)
-      __hip_atomic_store(&S->chain_claim[threadIdx.x][0], static_cast<uint64_t>(epoch) << 32,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
     if (has_prev) {
       if constexpr (MODE == kChainFin) {
         const Consts Kp = S->h.K;
@@ -675,18 +665,7 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
   // the last control loads, so the end of the loop normally finds them there.
   uint64_t w_pre = 0;
   bool pre_issued = false;
-#if MPC_CHAIN_XCLAIM
-  uint32_t xcc = 0;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  xcc &= 7u;
-  uint64_t claim_old = 0;   // thread 0: own pool's claim, issued with the tile's last loads
-#endif
   auto mid = [&]() {
-#if MPC_CHAIN_XCLAIM
-    if (threadIdx.x == 0)
-      claim_old = __hip_atomic_fetch_add(&S->chain_claim[xcc][0], 1ull, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-#endif
     if (waited || pre_issued || s_final) return;
     pre_issued = true;
     if (threadIdx.x < kPubWords)
@@ -721,95 +700,6 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
   const int64_t n_tiles = (n_cand + kBlock * CPL - 1) / (kBlock * CPL);
   uint64_t best_k = ~0ull;
   int64_t best_i = INT64_MAX;
-#if MPC_CHAIN_XCLAIM
-  // One resident round of blocks (the host sizes the grid): block b rolls out
-  // tile b - 1; the second round's tiles are dealt into 8 pools (pool p: tiles
-  // G1 + p + 8c) and a block claims from its own XCD's pool (the claim issued
-  // with its tile's last loads), then steals from the pool with the most left.
-  {
-    __shared__ int64_t s_next;
-    const int64_t G1 = gridDim.x - 1;
-    const int64_t T2 = n_tiles > G1 ? n_tiles - G1 : 0;
-    auto pool_size = [&](int p) -> int64_t { return T2 > p ? (T2 - p + 7) / 8 : 0; };
-    int64_t tile = blockIdx.x - 1;
-    while (tile < n_tiles) {
-      const int64_t c0 = tile * (kBlock * CPL) + threadIdx.x * CPL;
-      const int64_t cl = c0 < n_cand ? c0 : n_cand - CPL;
-      double cst[CPL];
-      rollout_lane_glds_k<INTEG, ROT, PL2, decltype(wait), decltype(pre0), decltype(mid),
-                          MPC_CHAIN_PIN>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0, mid);
-      Kl = K;
-      if (c0 < n_cand) {
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) {
-          const uint64_t kk = cost_key(cst[j]);
-          if (rec_less(kk, c0 + j, best_k, best_i)) {
-            best_k = kk;
-            best_i = c0 + j;
-          }
-        }
-      }
-      if (threadIdx.x == 0) {
-        if (n_steps < 3)   // (no mid() call: claim now)
-          claim_old = __hip_atomic_fetch_add(&S->chain_claim[xcc][0], 1ull, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-        int64_t next = n_tiles;
-        int pool = static_cast<int>(xcc);
-        uint64_t w = claim_old;
-        for (uint32_t it = 0; it < kChainSpinLimit; ++it) {
-          if (static_cast<uint32_t>(w >> 32) == epoch) {
-            const int64_t c = static_cast<int64_t>(static_cast<uint32_t>(w));
-            if (c < pool_size(pool)) {
-              next = G1 + pool + 8 * c;
-              break;
-            }
-            // this pool is empty: the pool with the most tiles left, if any
-            uint64_t q[8];
-#pragma unroll
-            for (int p = 0; p < 8; ++p)
-              q[p] = __hip_atomic_load(&S->chain_claim[p][0], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            int64_t best_left = 0;
-            pool = -1;
-#pragma unroll
-            for (int p = 0; p < 8; ++p) {
-              const int64_t left = static_cast<uint32_t>(q[p] >> 32) == epoch
-                                       ? pool_size(p) - static_cast<int64_t>(static_cast<uint32_t>(q[p]))
-                                       : pool_size(p);
-              if (left > best_left) {
-                best_left = left;
-                pool = p;
-              }
-            }
-            if (pool < 0) break;                       // every pool drained
-          } else {
-            __builtin_amdgcn_s_sleep(8);               // block 0 has not reset yet
-            if (static_cast<uint32_t>(__hip_atomic_load(&S->chain_claim[pool][0], __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT) >> 32) != epoch)
-              continue;
-          }
-          w = __hip_atomic_fetch_add(&S->chain_claim[pool][0], 1ull, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-        }
-        s_next = next;
-      }
-      __syncthreads();
-      tile = s_next;
-      __syncthreads();   // s_next is rewritten by the next tile
-    }
-  }
-  block_argmin(best_k, best_i);
-  if (threadIdx.x == 0) {
-    part[blockIdx.x - 1] = Rec{best_k, best_i};
-    // the consumers reduce the records of a tile-per-block grid: the slots
-    // this shorter grid does not own hold the empty record
-    const int64_t n_rec = n_tiles < kMaxBlocks ? n_tiles : kMaxBlocks;
-    for (int64_t s = blockIdx.x - 1 + (gridDim.x - 1); s < n_rec; s += gridDim.x - 1)
-      part[s] = Rec{~0ull, INT64_MAX};
-  }
-  MPC_TL(4);
-  return;
-#endif
   for (int64_t tile = blockIdx.x - 1; tile < n_tiles; tile += gridDim.x - 1) {
     const int64_t c0 = tile * (kBlock * CPL) + threadIdx.x * CPL;
     // lanes past the end of a partial tile roll the last pair again (result

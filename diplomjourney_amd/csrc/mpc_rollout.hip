@@ -149,30 +149,6 @@ int64_t fused_grid(int64_t n_cand) {
   return std::max<int64_t>(1, std::min(cdiv(n_cand, kBlock * CPL), cache[dev]));
 }
 
-#if MPC_CHAIN_XCLAIM
-// Resident blocks of the chained kernel (occupancy x CUs), cached per device;
-// all instantiations share its register and LDS budget.
-int64_t chain_resident() {
-  static int64_t cache[16] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
-  if (cache[dev] == 0) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu,
-            reinterpret_cast<const void*>(&k_episode_chain<MPC_INTEG_RECT, kRotCum, 1, true>),
-            kBlock, 0) != hipSuccess ||
-        per_cu < 1)
-      per_cu = 1;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus < 1)
-      cus = 256;
-    cache[dev] = std::max<int64_t>(2, static_cast<int64_t>(per_cu) * cus);
-  }
-  return cache[dev];
-}
-#endif
-
 // Number of block records the rollout launch for these arguments writes
 // (= its grid); the finalize launch reduces exactly these.
 int64_t partial_count(const double* v_sc, const double* beta_sc, int64_t n_cand,
@@ -569,13 +545,7 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
   EpisodeState* S = static_cast<EpisodeState*>(state);
   int e;
   const int pl2 = frexp(cfg->L, &e) == 0.5 ? 1 : 0;   // as consts_from_problem decides
-#if MPC_CHAIN_XCLAIM
-  // one resident round (block 0 included); the records of the tile-per-block
-  // grid beyond it are filled with the empty record by the kernel
-  const int64_t grid = std::min<int64_t>(rollout_grid<kCplWide>(n_cand), chain_resident() - 1) + 1;
-#else
   const int64_t grid = rollout_grid<kCplWide>(n_cand) + 1;
-#endif
   const int n_part_prev = static_cast<int>(rollout_grid<kCplWide>(n_cand));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   constexpr int I = MPC_INTEG_RECT;
