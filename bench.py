@@ -335,10 +335,56 @@ def main():
         "generated_inputs": generated,
         "cpu_baseline": cpu,
     }
+    if out["roofline"] is not None and pool is not None:
+        # the same kernel against a measured copy ceiling and
+        # its VALU issue share (PMC counters of the committed traffic summary)
+        ceil = copy_ceiling(pool)
+        out["roofline"]["copy_ceiling_GBs"] = ceil
+        out["roofline"]["frac_of_copy_ceiling"] = achieved / ceil
+        out["roofline"]["valu"] = valu_share(args.traffic_json, kernel, bytes_launch, kern_ms)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1 or args.exchange:
         dist.destroy_process_group()
+
+
+def copy_ceiling(pool, reps=20):
+    """Measured HBM ceiling on this GPU: device-to-device copies of the
+    resident batches' v rows into a scratch buffer (rotating over the pool, so
+    no source is cache-resident), HIP events; GB/s of bytes read + written."""
+    import torch
+    src = [v for v, _ in pool]
+    dst = torch.empty_like(src[0])
+    for i in range(4):
+        dst.copy_(src[i % len(src)])
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(reps):
+        dst.copy_(src[(i + 1) % len(src)])
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del dst
+    return 2.0 * src[0].numel() * 8 / (ms * 1e-3) / 1e9
+
+
+def valu_share(traffic_json, kernel, bytes_launch, kern_ms):
+    """VALU wave-instructions per launch (SQ_INSTS_VALU, PMC) and the share of
+    the fp64 issue rate they take: 4 cycles per wave-instruction on each of the
+    1024 SIMDs at 2.4 GHz (78.6 TFLOP/s of fp64 FMA); integer and fp32 VALU
+    instructions are counted as fp64 ones, so the share is an upper bound."""
+    path = traffic_json or (os.path.join(REPO, "profiles", TRAFFIC_JSON[kernel])
+                            if kernel in TRAFFIC_JSON else None)
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        t = json.load(fh)
+    insts = t.get("counters_median_per_launch", {}).get("SQ_INSTS_VALU")
+    if (insts is None or t.get("kernel", kernel) != kernel
+            or abs(t.get("algorithmic_bytes_per_launch", -1) - bytes_launch) >= 1):
+        return None
+    return {"wave_insts_per_launch": insts, "source": os.path.relpath(path, REPO),
+            "fp64_issue_share": insts * 4.0 / (1024 * 2.4e9 * kern_ms * 1e-3)}
 
 
 INPUTS_DOC = {

@@ -734,6 +734,10 @@ def test_bench_contract(extra):
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] < 1
     assert rf["algorithmic_bytes_per_launch"] == 16.0 * 10 * 1_000_000
+    # a measured copy ceiling beside the spec peak, and the
+    # kernel's VALU issue share from the committed PMC counters
+    assert 2000 < rf["copy_ceiling_GBs"] < 9000 and 0 < rf["frac_of_copy_ceiling"] < 1.5
+    assert 0 < rf["valu"]["fp64_issue_share"] < 1.5
     if extra:
         assert d["config"]["integrator"] == "rect+rot"
         assert rf["kernel"] == "k_rollout_argmin_stream"
