@@ -521,7 +521,8 @@ template <int INTEG, int ROT>
 __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
                             const double* __restrict__ b, int64_t ld, int n_steps, uint64_t key,
                             int64_t col, int64_t reported_index, double incumbent,
-                            mpc_result_t* __restrict__ out, Winner* win = nullptr) {
+                            mpc_result_t* __restrict__ out, Winner* win = nullptr,
+                            const double* pre_v = nullptr, const double* pre_b = nullptr) {
   __shared__ double s_v[MPC_MAX_STEPS], s_dphi[MPC_MAX_STEPS], s_phi[MPC_MAX_STEPS];
   __shared__ double s_a[MPC_MAX_STEPS], s_c[MPC_MAX_STEPS];
   __shared__ double s_b0;
@@ -544,8 +545,10 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
   // exactly as rollout_candidate / the rollout kernels decide.
   double vs = 0.0, w = 0.0, bs = 0.0;
   if (valid && lane < n_steps) {
-    vs = v[lane * ld + col];
-    bs = b[lane * ld + col];
+    // pre_v / pre_b: the winner's controls already staged in LDS by the caller
+    // (finalize_block prefetches each wave's best during the block reduction)
+    vs = pre_v ? pre_v[lane] : v[lane * ld + col];
+    bs = pre_b ? pre_b[lane] : b[lane * ld + col];
     s_v[lane] = vs;
     if (lane == 0) s_b0 = bs;
     w = K.L_pow2 ? vs * K.inv_L : vs / K.L;
@@ -795,18 +798,41 @@ __device__ __forceinline__ void finalize_block(
   if (KDEV && hook.H && threadIdx.x >= 64 && threadIdx.x < 64 + kHeadWords)
     s_head[threadIdx.x - 64] = reinterpret_cast<const uint64_t*>(hook.H)[threadIdx.x - 64];
   wave_argmin(k, i);
-  if ((threadIdx.x & 63) == 0) {
+  // Each wave's best candidate's controls, loaded while the waves' minima are
+  // combined: the block's winner is one of them, so its re-roll starts
+  // without a dependent load of its own (one memory round trip fewer on the
+  // selection's critical path; the same values, so the same arithmetic).
+  __shared__ double s_pv[MPC_MAX_STEPS], s_pb[MPC_MAX_STEPS];
+  double pv = 0.0, pb = 0.0;
+  const int ln = threadIdx.x & 63;
+  if constexpr (!GEN) {
+    if (k != ~0ull && ln < n_steps) {
+      pv = v[ln * n_cand + i];
+      pb = b[ln * n_cand + i];
+    }
+  }
+  if (ln == 0) {
     s_key[threadIdx.x >> 6] = k;
     s_idx[threadIdx.x >> 6] = i;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < NT / 64; ++w)
-      if (rec_less(s_key[w], s_idx[w], k, i)) {
-        k = s_key[w];
-        i = s_idx[w];
-      }
-  }
+  // every thread forms the block's winner (thread 0's result as before), so
+  // the wave that holds it knows to stage its controls
+  int wbest = 0;
+  k = s_key[0];
+  i = s_idx[0];
+  for (int w = 1; w < NT / 64; ++w)
+    if (rec_less(s_key[w], s_idx[w], k, i)) {
+      k = s_key[w];
+      i = s_idx[w];
+      wbest = w;
+    }
+  if constexpr (!GEN) {
+    if ((threadIdx.x >> 6) == wbest && ln < n_steps) {
+      s_pv[ln] = pv;
+      s_pb[ln] = pb;
+    }
+  }   // (emit_winner's first barrier orders these stores before its reads)
 #ifdef MPC_FIN_TRACE
   const uint64_t tr1 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -817,7 +843,8 @@ __device__ __forceinline__ void finalize_block(
     const int64_t col = k == ~0ull ? 0 : ((i / (kBlock * 2)) % n_part) * MPC_MAX_STEPS;
     emit_winner<INTEG, ROT>(K, v, b, 1, n_steps, k, col, index_base + i, incumbent, out, &w);
   } else {
-    emit_winner<INTEG, ROT>(K, v, b, n_cand, n_steps, k, i, index_base + i, incumbent, out, &w);
+    emit_winner<INTEG, ROT>(K, v, b, n_cand, n_steps, k, i, index_base + i, incumbent, out, &w,
+                            s_pv, s_pb);
   }
 #ifdef MPC_FIN_TRACE
   const uint64_t tr2 = __builtin_amdgcn_s_memrealtime();
