@@ -111,10 +111,6 @@ def parse():
     ap.add_argument("--no-chain", action="store_true",
                     help="separate selection launch per step instead of chained steps "
                          "(mpc_episode_chain_step: the step's launch completes the previous step)")
-    ap.add_argument("--run", action="store_true",
-                    help="persistent run: the K timed steps in ONE launch (mpc_episode_run; "
-                         "rect+cum, one GPU, resident inputs): step j+1's tiles stream while "
-                         "step j is being selected")
     ap.add_argument("--no-graph", action="store_true",
                     help="time eagerly launched steps instead of a HIP graph replay")
     ap.add_argument("--exchange", action="store_true",
@@ -233,35 +229,24 @@ def main():
                            chain=not args.no_chain and args.integrator == "rect+cum",
                            generate=inputs == "generated")
     pool = make_pool(eng, ep, n_steps, args.steps) if inputs == "resident" else None
-    persistent = args.run
     rollout_ms = None
     # the launch that carries the step: the chained kernel (rollout of step k +
-    # completion of step k-1), the persistent run, or the rollout kernel
-    chained = (not persistent and not exchange and getattr(ep, "chain", False)
-               and inputs == "resident")
-    kernel = ("k_episode_run" if persistent else
-              "k_episode_chain" if chained else "k_rollout_argmin_stream")
-    if persistent and (exchange or args.host_loop or inputs != "resident"
-                       or args.integrator != "rect+cum"):
-        raise SystemExit("--run: one GPU, resident inputs, --integrator rect+cum")
-    if persistent:
-        main_run = run_persistent(args, ep, pool, world, device)
-        use_graph = False
-        kern_ms = main_run["kernel_ms"]
-    else:
-        main_run = run_steps(args, ep, pool, use_graph, world, device)
-        use_graph = main_run["graph"]
-        kern_ms = main_run["kernel_in_step_ms"]
-        if chained:
-            kern_ms = chain_pass(ep, pool)
-            # for comparison: the same controls through the rollout kernel alone
-            # (the chained launch adds block 0's completion of the previous step)
-            rollout_ms = kernel_pass(ep, pool)
-        elif inputs == "generated":
-            pass   # events around the generated rollout + selection (no HBM roofline)
-        elif hasattr(ep, "partials"):
-            kern_ms = kernel_pass(ep, pool if pool is not None else
-                                  make_pool(eng, ep, n_steps, 4))
+    # completion of step k-1) or the rollout kernel
+    chained = not exchange and getattr(ep, "chain", False) and inputs == "resident"
+    kernel = "k_episode_chain" if chained else "k_rollout_argmin_stream"
+    main_run = run_steps(args, ep, pool, use_graph, world, device)
+    use_graph = main_run["graph"]
+    kern_ms = main_run["kernel_in_step_ms"]
+    if chained:
+        kern_ms = chain_pass(ep, pool)
+        # for comparison: the same controls through the rollout kernel alone
+        # (the chained launch adds block 0's completion of the previous step)
+        rollout_ms = kernel_pass(ep, pool)
+    elif inputs == "generated":
+        pass   # events around the generated rollout + selection (no HBM roofline)
+    elif hasattr(ep, "partials"):
+        kern_ms = kernel_pass(ep, pool if pool is not None else
+                              make_pool(eng, ep, n_steps, 4))
     other = generated = None
     if not args.host_loop and not args.no_second_pass:
         # the other input mode, same episode machinery, for comparison
@@ -280,7 +265,7 @@ def main():
                          "ms_per_step": r["elapsed"] / args.steps * 1e3,
                          "p50_ms": r["p50_ms"]}
     elapsed = main_run["elapsed"]
-    bytes_launch = 16.0 * n_steps * ep.n_local * (args.steps if persistent else 1)
+    bytes_launch = 16.0 * n_steps * ep.n_local
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     value = n_total * args.steps / elapsed
     if not args.host_loop:
@@ -304,16 +289,10 @@ def main():
                    "integrator": args.integrator, "inputs": INPUTS_DOC[inputs],
                    "episodes_started": episodes,
                    "episode_loop": "host" if args.host_loop else "device-resident",
-                   "launch": ("one persistent launch of the K steps (mpc_episode_run)"
-                              if persistent else
-                              (("hipGraph of the K steps" + (" incl. the RCCL all_gather"
-                                                             if exchange else ""))
-                               if use_graph else "eager")),
-                   "step_launches": ("persistent: units of 512 candidates claimed in order "
-                                     "across steps; block 0 selects step j (records, winner "
-                                     "re-roll, episode update) while step j+1 streams"
-                                     if persistent else
-                                     ("chained: rollout of step k + completion of step k-1 in "
+                   "launch": (("hipGraph of the K steps" + (" incl. the RCCL all_gather"
+                                                            if exchange else ""))
+                              if use_graph else "eager"),
+                   "step_launches": (("chained: rollout of step k + completion of step k-1 in "
                                       "one launch" + (" (+ local finalize + all_gather)"
                                                       if exchange else ""))
                                      if getattr(ep, "chain", False) and inputs == "resident"
@@ -322,9 +301,7 @@ def main():
                    "parallelism": f"candidate-sharded x{world}" + (", all_gather(808 B)/step"
                                                                    if exchange else "")},
         "p50_ms": main_run["p50_ms"], "p90_ms": main_run["p90_ms"],
-        "p50_note": ("MPC-step period: device clock between consecutive step completions "
-                     "(selection published) inside the timed persistent launch" if persistent else
-                     "GPU time per MPC step (HIP events between step starts, eager launches)"),
+        "p50_note": "GPU time per MPC step (HIP events between step starts, eager launches)",
         "kernel_ms": kern_ms, "kernel_in_step_ms": main_run["kernel_in_step_ms"],
         "roofline": (None if inputs == "generated" else
                      roofline(achieved, bytes_launch, args.traffic_json, kernel=kernel)),
@@ -505,43 +482,6 @@ def run_steps(args, ep, pool, use_graph, world, device):
             "p50_ms": percentile(step_gpu_ms, 50),
             "p90_ms": percentile(step_gpu_ms, 90),
             "kernel_in_step_ms": sum(a.elapsed_time(b) for a, b in kern) / len(kern)}
-
-
-def run_persistent(args, ep, pool, world, device):
-    """The K timed steps as one persistent launch (mpc_episode_run): warmup
-    launch of W steps, then the timed launch between a barrier + sync on
-    both sides.  kernel_ms = HIP events around the timed launch on its stream
-    (the run workspace's memset node + the kernel); the MPC-step period comes
-    from the device clock each step's selection writes when it publishes."""
-    import torch
-    import torch.distributed as dist
-    from diplomjourney_amd.episode import percentile
-    K, W = args.steps, args.warmup
-    batches = [pool[i % len(pool)] for i in range(K)]
-    if W:
-        ep.run([pool[i % len(pool)] for i in range(W)])
-    ep._ptr_table(batches[:ep.log_capacity])          # pointer table uploaded untimed
-    clock = torch.zeros(K, dtype=torch.int64, device=device)
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    e0.record()
-    ep.run(batches, clock=clock)
-    e1.record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    assert ep.chain_error() == 0, "persistent run: a bounded wait timed out"
-    ticks = clock.cpu().tolist()
-    period_ms = [(b - a) * 1e-5 for a, b in zip(ticks, ticks[1:])]   # 100 MHz ticks
-    return {"elapsed": elapsed, "graph": False, "p50_ms": percentile(period_ms, 50),
-            "p90_ms": percentile(period_ms, 90), "kernel_ms": e0.elapsed_time(e1),
-            "kernel_in_step_ms": e0.elapsed_time(e1) / K}
 
 
 def kernel_pass(ep, pool, reps=100, warm=200):

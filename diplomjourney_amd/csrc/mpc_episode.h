@@ -232,13 +232,11 @@ __device__ __forceinline__ void generated_lane(const Consts& K, const double2* s
   }
 }
 
-#ifndef MPC_GEN_WAVES
-#define MPC_GEN_WAVES 4   // launch bound of the generated-controls rollout
-#endif
+constexpr int kGenWaves = 4;   // launch bound of the generated-controls rollout (5 spills)
 // PL2 (wheelbase a power of two) is a template parameter picked by the host
 // from cfg, as in the chained step (one rollout variant per kernel).
 template <int INTEG, int ROT, bool PL2>
-__global__ __launch_bounds__(kBlock, MPC_GEN_WAVES) void k_rollout_generated(
+__global__ __launch_bounds__(kBlock, kGenWaves) void k_rollout_generated(
     mpc_episode_config_t c, EpisodeState* __restrict__ S, int64_t n_cand, int n_steps,
     int64_t base, Rec* __restrict__ part, double* __restrict__ part_v,
     double* __restrict__ part_b) {
@@ -401,13 +399,7 @@ __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeHea
     const double ex = S->x_t - S->x, ey = S->y_t - S->y;
     if (ex * ex + ey * ey <= c.eps || S->p > c.max_steps) episode_restart(c, *S);
   }
-#ifdef MPC_FIN_TRACE
-  g_fin_tick[1] = __builtin_amdgcn_s_memrealtime();
-#endif
   episode_prepare(c, *S);
-#ifdef MPC_FIN_TRACE
-  g_fin_tick[2] = __builtin_amdgcn_s_memrealtime();
-#endif
   L.x = S->x;
   L.y = S->y;
   L.phi = S->phi;
@@ -557,35 +549,13 @@ __device__ __forceinline__ bool chain_read(const EpisodeState* S, uint32_t epoch
   return __ballot(!ok) == 0;
 }
 
-#ifndef MPC_CHAIN_WAVES
-#define MPC_CHAIN_WAVES 5   // launch bound of the chained kernel: waves per SIMD
-#endif
-#ifndef MPC_CHAIN_PIN
-#define MPC_CHAIN_PIN false
-#endif
-#ifdef MPC_CHAIN_TIMELINE
-// Debug builds only (tools/chain_timeline.py): per block of the last chained
-// launch, s_memrealtime ticks (100 MHz) at entry, once its first control
-// DMAs are in flight and the constants read (pre0), at the loop's end, after
-// the final constants (wait) and after its record; plus its XCC id.
-constexpr int kTlBlocks = 8192;
-__device__ uint64_t g_chain_tl[kTlBlocks][6];
-#define MPC_TL(slot)                                                                \
-  do {                                                                              \
-    if (threadIdx.x == 0 && blockIdx.x < kTlBlocks)                                 \
-      g_chain_tl[blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime();              \
-  } while (0)
-#else
-#define MPC_TL(slot) \
-  do {               \
-  } while (0)
-#endif
+constexpr int kChainWaves = 5;   // launch bound of the chained kernel: waves per SIMD
 
 // PL2 (wheelbase a power of two) is a template parameter, not a runtime
 // branch: with both rollout variants inlined the kernel held 119 VGPRs and
 // spilled 191 SGPRs; one variant per instantiation: 108-112 VGPRs, 81-86.
 template <int INTEG, int ROT, int MODE, bool PL2>
-__global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
+__global__ __launch_bounds__(kBlock, kChainWaves) void k_episode_chain(
     EpisodeState* __restrict__ S, uint32_t epoch, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part,
     int has_prev, const Rec* __restrict__ part_prev, int n_part_prev,
@@ -593,14 +563,6 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
     mpc_result_t* __restrict__ out_prev, const mpc_result_t* __restrict__ gathered,
     int n_gathered, mpc_episode_config_t ecfg, mpc_episode_log_t* __restrict__ log, int cap) {
   static_assert(ROT == kRotCum, "chained steps need the pose-independent recurrence");
-  MPC_TL(0);
-#ifdef MPC_CHAIN_TIMELINE
-  if (threadIdx.x == 0) {
-    uint32_t xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    g_chain_tl[blockIdx.x][5] = xcc;
-  }
-#endif
   if (blockIdx.x == 0) {
     if (has_prev) {
       if constexpr (MODE == kChainFin) {
@@ -620,7 +582,6 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
     // wrong form: flag it (chain_error = 2) instead of returning wrong costs
     // silently.  (chain_publish ended with a barrier after the head store.)
     if (threadIdx.x == 0 && (S->h.K.L_pow2 != 0) != PL2) S->chain_error = 2u;
-    MPC_TL(4);
     return;
   }
   constexpr int CPL = 2;
@@ -642,7 +603,6 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
       if (threadIdx.x == 0) s_final = fin;
     }
     __syncthreads();
-    MPC_TL(1);
     Kl = consts_from_words(s_w);
     if (s_final) return;
     // speculate h from the published t: the previous step's (+ dt) or, if
@@ -677,7 +637,6 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
   auto wait = [&]() {
     if (waited) return;
     waited = true;
-    MPC_TL(2);
     __syncthreads();   // LDS reuse
     if (!s_final) {
       if (threadIdx.x < 64) {
@@ -695,7 +654,6 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
       __syncthreads();
     }
     K = consts_from_words(s_w);
-    MPC_TL(3);
   };
   const int64_t n_tiles = (n_cand + kBlock * CPL - 1) / (kBlock * CPL);
   uint64_t best_k = ~0ull;
@@ -709,7 +667,7 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
     // leading trig coefficients not pinned: the fifth wave per SIMD needs the
     // registers more (as the rect+cum stream kernel)
     rollout_lane_glds_k<INTEG, ROT, PL2, decltype(wait), decltype(pre0), decltype(mid),
-                        MPC_CHAIN_PIN>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0, mid);
+                        false>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0, mid);
     Kl = K;            // later tiles: the final constants
     if (c0 < n_cand) {
 #pragma unroll
@@ -724,7 +682,6 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_WAVES) void k_episode_chain(
   }
   block_argmin(best_k, best_i);
   if (threadIdx.x == 0) part[blockIdx.x - 1] = Rec{best_k, best_i};
-  MPC_TL(4);
 }
 
 }  // namespace mpc

@@ -30,35 +30,12 @@
 namespace mpc {
 
 constexpr int kBlock = 256;  // 4 waves of 64
-// Build-time tuning knobs (A/B-tested with tools/probe_gpu.py variants):
-#ifndef MPC_CPL
-#define MPC_CPL 2            // candidates per lane on the aligned path (2 or 4)
-#endif
-#ifndef MPC_PREFETCH
-#define MPC_PREFETCH 2       // control-load pipeline depth in steps (>= 2)
-#endif
-#ifndef MPC_GLDS
-#define MPC_GLDS 1           // wide path: LDS-DMA control ring (0: register ring)
-#endif
-#ifndef MPC_EXPERIMENT
-#define MPC_EXPERIMENT 0     // A/B probes only: 1 = loads without the step math, 2 = math without loads
-#endif
-#ifndef MPC_MIN_WAVES
-#define MPC_MIN_WAVES 1      // __launch_bounds__ minimum waves per SIMD
-#endif
-constexpr int kCplWide = MPC_CPL;
-static_assert(kCplWide == 2 || kCplWide == 4, "MPC_CPL must be 2 or 4");
-constexpr int kPrefetch = MPC_PREFETCH;
-static_assert(kPrefetch >= 2, "MPC_PREFETCH must be >= 2");
+// Tuning constants (DESIGN.md §5 records the A/B measurements behind them).
+constexpr int kCplWide = 2;    // candidates per lane on the aligned path (16-B control loads)
+constexpr int kPrefetch = 2;   // register-ring depth in steps of the scalar / states path
 constexpr int kWaves = kBlock / 64;
-#ifndef MPC_MAX_BLOCKS
-#define MPC_MAX_BLOCKS 2048   // A/B probes cap the rollout grid lower
-#endif
-constexpr int64_t kMaxBlocks = MPC_MAX_BLOCKS;  // 256 CUs x 8 resident blocks upper bound
-#ifndef MPC_FIN_BLOCK
-#define MPC_FIN_BLOCK 256    // threads of the one-block finalize kernels (A/B: 1024 -> 256 = -0.7 us)
-#endif
-constexpr int kFinBlock = MPC_FIN_BLOCK;
+constexpr int64_t kMaxBlocks = 2048;   // rollout grid cap: 256 CUs x 8 resident blocks
+constexpr int kFinBlock = 256;         // one-block selection kernels (A/B: 1024 -> 256 = -0.7 us)
 
 struct Rec {
   uint64_t key;
@@ -99,14 +76,6 @@ __device__ __forceinline__ void rollout_lane_l(const Consts& K, const double* __
   // Controls of step sr for this lane's CPL candidates: 16 B per lane per
   // array on the wide path (one 1 KiB wave-instruction each).
   auto load = [&](int sr, double (&vv)[CPL], double (&bb)[CPL]) {
-#if MPC_EXPERIMENT == 2
-#pragma unroll
-    for (int h = 0; h < CPL; ++h) {
-      vv[h] = 0.5 + 1e-3 * static_cast<double>((c0 + h + sr) & 15);
-      bb[h] = 0.01 * static_cast<double>(((c0 + h) >> 4) & 31) - 0.15;
-    }
-    return;
-#endif
     if constexpr (CPL >= 2) {
 #pragma unroll
       for (int h = 0; h < CPL; h += 2) {
@@ -128,11 +97,6 @@ __device__ __forceinline__ void rollout_lane_l(const Consts& K, const double* __
   auto body = [&](int sr, const double (&vv)[CPL], const double (&bb)[CPL]) {
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
-#if MPC_EXPERIMENT == 1
-      x[j] = x[j] + vv[j] * bb[j];
-      y[j] = y[j] + vv[j];
-      continue;
-#endif
       step_core<INTEG, ROT, PL2>(x[j], y[j], ph[j], sn[j], cs[j], vv[j], bb[j], K, bad[j]);
       if constexpr (STATES) {
         double px = x[j], py = y[j];
@@ -200,14 +164,9 @@ __device__ __forceinline__ void rollout_lane_l(const Consts& K, const double* __
 // orders against the LDS reads: the waits are explicit (vmcnt for "slot
 // landed", lgkmcnt(0) before a slot is refilled) and every asm statement
 // clobbers memory.
-#ifndef MPC_GLDS_POLICY
-#define MPC_GLDS_POLICY " nt"   // control DMA is streamed once: non-temporal (A/B: -1.5 us/step on config C)
-#endif
-#ifndef MPC_RING
-#define MPC_RING 3           // LDS ring depth in steps (kRing-1 steps in flight)
-#endif
-constexpr int kRing = MPC_RING;
-static_assert(kRing >= 2 && kRing <= 8, "MPC_RING must be in [2, 8]");
+// The control DMA is streamed once: non-temporal (A/B: -1.5 us/step on config C).
+#define MPC_GLDS_POLICY " nt"
+constexpr int kRing = 3;   // LDS ring depth in steps (kRing-1 steps in flight)
 
 // One ring for every instantiation (namespace scope: allocated once per kernel).
 __shared__ double2 g_ring[kWaves][kRing][2][64];  // [wave][slot][v|beta][lane]
@@ -326,7 +285,7 @@ __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Const
   for (int pass = 0;; ++pass) {
 #pragma unroll
     for (int u = 0; u < R - 1; ++u)
-      if (u < n_steps && MPC_EXPERIMENT != 2)
+      if (u < n_steps)
         glds_pair(v + u * ld + c0, b + u * ld + c0, dst(u), dst(u) + kSlot / 2);
     if (pass == 0) {
       if constexpr (ROT != kRotCum)
@@ -347,8 +306,7 @@ __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Const
       for (int u = 0; u < R; ++u) {
         const int st = s + u;
         if (st < n_steps) {
-          if (MPC_EXPERIMENT == 2) {
-          } else if (st + R - 1 < n_steps) {
+          if (st + R - 1 < n_steps) {
             const int sr = st + R - 1, slot = (u + R - 1) % R;   // = the slot read last step
             glds_refill(v + sr * ld + c0, b + sr * ld + c0, dst(slot), dst(slot) + kSlot / 2, v2,
                         b2);
@@ -361,14 +319,6 @@ __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Const
           }
           v2 = g_ring[wv][u][0][lane];
           b2 = g_ring[wv][u][1][lane];
-#if MPC_EXPERIMENT == 1
-          x[0] += v2.x * b2.x;
-          x[1] += v2.y * b2.y;
-          continue;
-#elif MPC_EXPERIMENT == 2
-          v2 = make_double2(0.5 + 1e-3 * ((c0 + st) & 15), 0.5 + 1e-3 * ((c0 + 1 + st) & 15));
-          b2 = make_double2(0.01 * ((c0 >> 4) & 31) - 0.15, 0.01 * (((c0 + 1) >> 4) & 31) - 0.15);
-#endif
           // the heading itself is not needed here (rotation mode carries sin/cos;
           // an irregular candidate is recomputed from K.phi), so no phi chain
           double ph0 = ROT ? 0.0 : ph[0], ph1 = ROT ? 0.0 : ph[1];
@@ -430,7 +380,6 @@ __device__ __forceinline__ void rollout_lane(const Consts& K, const double* __re
                                              const double* __restrict__ b, int64_t ld, int64_t c0,
                                              int n_steps, double (&cst)[CPL],
                                              double* __restrict__ states, int64_t n_cand) {
-#if MPC_GLDS
   if constexpr (CPL == 2 && !STATES) {
     if (K.L_pow2)
       rollout_lane_glds<INTEG, ROT, true>(K, v, b, ld, c0, n_steps, cst);
@@ -438,7 +387,6 @@ __device__ __forceinline__ void rollout_lane(const Consts& K, const double* __re
       rollout_lane_glds<INTEG, ROT, false>(K, v, b, ld, c0, n_steps, cst);
     return;
   }
-#endif
   if (K.L_pow2)
     rollout_lane_l<CPL, INTEG, ROT, STATES, true>(K, v, b, ld, c0, n_steps, cst, states, n_cand);
   else
@@ -475,7 +423,7 @@ __device__ __forceinline__ void rollout_argmin_body(
 
 // Scalar (CPL = 1), CoordinateTree-states and register-ring paths.
 template <int CPL, int INTEG, int ROT, bool STATES, bool KDEV>
-__global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(
+__global__ __launch_bounds__(kBlock, 1) void k_rollout_argmin(
     Consts Karg, const Consts* __restrict__ Kdev, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part,
     double* __restrict__ states) {
@@ -487,11 +435,9 @@ __global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_argmin(
 // irregular-candidate recompute free of the device library's large-argument
 // trig (mpc_trig.h reduce_pio2_large), its registers fit kStreamWaves waves
 // per SIMD (5: <= 96 VGPRs; 6 spills).
-#ifndef MPC_STREAM_WAVES
-#define MPC_STREAM_WAVES 5
-#endif
+constexpr int kStreamWaves = 5;
 template <int INTEG, int ROT, bool KDEV>
-__global__ __launch_bounds__(kBlock, MPC_STREAM_WAVES) void k_rollout_argmin_stream(
+__global__ __launch_bounds__(kBlock, kStreamWaves) void k_rollout_argmin_stream(
     Consts Karg, const Consts* __restrict__ Kdev, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part) {
   rollout_argmin_body<kCplWide, INTEG, ROT, false, KDEV>(Karg, Kdev, v, b, n_cand, n_steps,
@@ -731,9 +677,6 @@ __device__ __forceinline__ void load8_rec_sc1(const Rec* const (&p)[8], u64x2 (&
       : "memory");
 }
 
-#ifdef MPC_FIN_TRACE
-__device__ uint64_t g_fin_tick[4];   // debug builds only: stage ticks inside the hook
-#endif
 // GEN (generated controls, k_rollout_generated): v / b are [n_part][MPC_MAX_STEPS]
 // — the controls of each rollout block's best candidate — instead of the
 // [n_steps][n_cand] candidate arrays; the winner's are those of its block.
@@ -743,9 +686,6 @@ __device__ __forceinline__ void finalize_block(
     const double* __restrict__ b, int64_t n_cand, int n_steps, int64_t index_base,
     double incumbent, mpc_result_t* __restrict__ out, const mpc_episode_config_t& ecfg,
     const EpisodeHook& hook) {
-#ifdef MPC_FIN_TRACE
-  const uint64_t tr0 = __builtin_amdgcn_s_memrealtime();
-#endif
   // One-GPU episode: the episode scalars are staged in LDS by wave 1 (one
   // 8-B vector load per lane, issued after its record loads) and updated by
   // thread 0 once the winner is known.  (Loading them into thread 0's SGPRs
@@ -833,9 +773,6 @@ __device__ __forceinline__ void finalize_block(
       s_pb[ln] = pb;
     }
   }   // (emit_winner's first barrier orders these stores before its reads)
-#ifdef MPC_FIN_TRACE
-  const uint64_t tr1 = __builtin_amdgcn_s_memrealtime();
-#endif
   Winner w;
   if constexpr (GEN) {
     // (thread 0 holds the winner; emit_winner takes its column from thread 0)
@@ -846,16 +783,10 @@ __device__ __forceinline__ void finalize_block(
     emit_winner<INTEG, ROT>(K, v, b, n_cand, n_steps, k, i, index_base + i, incumbent, out, &w,
                             s_pv, s_pb);
   }
-#ifdef MPC_FIN_TRACE
-  const uint64_t tr2 = __builtin_amdgcn_s_memrealtime();
-#endif
   if (KDEV && hook.H) {
     if (threadIdx.x == 0) {   // emit_winner ended with a barrier
       EpisodeHead H;
       __builtin_memcpy(&H, s_head, sizeof(EpisodeHead));
-#ifdef MPC_FIN_TRACE
-      g_fin_tick[0] = __builtin_amdgcn_s_memrealtime();
-#endif
       episode_hook(ecfg, hook, w, H, s_log, s_slot);
       __builtin_memcpy(s_head, &H, sizeof(EpisodeHead));
     }
@@ -864,17 +795,6 @@ __device__ __forceinline__ void finalize_block(
     store_update(hook.H, s_head, s_slot, reinterpret_cast<const uint64_t*>(&s_log),
                  hook.chain_pub, hook.chain_pub_words);
   }
-#ifdef MPC_FIN_TRACE
-  if (threadIdx.x == 0) {   // debug builds only: 10-ns ticks in unused trajectory slots
-    const uint64_t tr3 = __builtin_amdgcn_s_memrealtime();
-    out->traj[31][0] = static_cast<double>(tr1 - tr0);
-    out->traj[31][1] = static_cast<double>(tr2 - tr1);
-    out->traj[31][2] = static_cast<double>(tr3 - tr2);
-    out->traj[30][0] = static_cast<double>(g_fin_tick[0] - tr2);
-    out->traj[30][1] = static_cast<double>(g_fin_tick[1] - g_fin_tick[0]);
-    out->traj[30][2] = static_cast<double>(g_fin_tick[2] - g_fin_tick[1]);
-  }
-#endif
 }
 
 // The selection of a generated-controls step (GEN finalize_block).
@@ -911,7 +831,7 @@ __global__ __launch_bounds__(kFinBlock) void k_finalize(
 // gridDim-1 is last, and its threads read every record `sc1` after a
 // workgroup barrier.  The last block re-arms the counter for the next launch.
 template <int CPL, int INTEG, int ROT>
-__global__ __launch_bounds__(kBlock, MPC_MIN_WAVES) void k_rollout_episode(
+__global__ __launch_bounds__(kBlock, 1) void k_rollout_episode(
     const Consts* __restrict__ Kdev, const double* __restrict__ v, const double* __restrict__ b,
     int64_t n_cand, int n_steps, int64_t index_base, Rec* __restrict__ part,
     uint32_t* __restrict__ done, const double* __restrict__ incumbent_dev,
@@ -1024,7 +944,7 @@ __device__ __forceinline__ Consts uniform_consts(const Consts& k) {
 // The wide variant runs the streaming kernel's lane (LDS-DMA ring): the same
 // 5 waves per SIMD (4 at the default bound: 120 VGPRs).
 template <int CPL, int INTEG, int ROT>
-__global__ __launch_bounds__(kBlock, CPL == kCplWide ? MPC_STREAM_WAVES : MPC_MIN_WAVES) void
+__global__ __launch_bounds__(kBlock, CPL == kCplWide ? kStreamWaves : 1) void
 k_rollout_argmin_batched(
     const mpc_problem_t* __restrict__ probs, const double* __restrict__ v,
     const double* __restrict__ b, int64_t cand, int n_steps, int64_t ld, Rec* __restrict__ part) {

@@ -18,7 +18,6 @@
 #include "mpc_episode.h"
 #include "mpc_fulltree.h"
 #include "mpc_kernels.h"
-#include "mpc_run.h"
 
 namespace mpc {
 namespace {
@@ -568,90 +567,6 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
   return last_hip_status();
 }
 
-// ----------------------------- persistent run --------------------------------
-static int64_t run_tiles(int64_t n_cand) { return cdiv(n_cand, kBlock * 2); }
-static size_t run_polled_bytes(int64_t n_cand) {
-  return sizeof(RunCtl) + static_cast<size_t>(2 * run_tiles(n_cand)) * kRunRecWords * 8;
-}
-
-size_t mpc_episode_run_workspace_bytes(int64_t n_cand, int32_t n_steps) {
-  (void)n_steps;
-  if (n_cand < 2) return 0;
-  return ((run_polled_bytes(n_cand) + 255) & ~static_cast<size_t>(255)) + sizeof(mpc_result_t);
-}
-
-int mpc_episode_run(const mpc_episode_config_t* cfg, void* state, const double* const* ctl,
-                    int32_t k_steps, int64_t n_cand, int32_t n_steps, int64_t index_base,
-                    int32_t integrator, void* ws, size_t ws_bytes, mpc_result_t* out,
-                    mpc_episode_log_t* log, int32_t log_capacity, uint64_t* step_clock,
-                    mpc_stream_t stream) {
-  if (check_episode_cfg(cfg) != MPC_OK || !state || !ctl || !out || k_steps < 1 ||
-      n_steps < 1 || n_steps > MPC_MAX_STEPS || index_base < 0 || log_capacity < 0)
-    return MPC_ERR_ARG;
-  // aligned path only (two candidates per lane); local indices travel as 32 bits
-  if (n_cand < 2 || n_cand % 2 != 0 || n_cand > 0x7fffffffll) return MPC_ERR_ARG;
-  if (run_tiles(n_cand) * static_cast<int64_t>(k_steps) > 0xffffffffll) return MPC_ERR_ARG;
-  // one log slot per step of the call (slots are not reused inside a launch)
-  if (log && log_capacity < k_steps) return MPC_ERR_ARG;
-  if (integrator != (MPC_INTEG_RECT | MPC_HEADING_CUMULATIVE)) return MPC_ERR_UNSUPPORTED;
-  if (!ws || ws_bytes < mpc_episode_run_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  char* w = static_cast<char*>(ws);
-  const size_t polled = run_polled_bytes(n_cand);
-  // every polled word zeroed before the launch (a memset node under capture)
-  if (hipMemsetAsync(w, 0, polled, st) != hipSuccess) return MPC_ERR_HIP;
-  RunCtl* rc = reinterpret_cast<RunCtl*>(w);
-  uint64_t* rec = reinterpret_cast<uint64_t*>(w + sizeof(RunCtl));
-  mpc_result_t* scratch =
-      reinterpret_cast<mpc_result_t*>(w + ((polled + 255) & ~static_cast<size_t>(255)));
-  EpisodeState* S = static_cast<EpisodeState*>(state);
-  int e;
-  const bool pl2 = frexp(cfg->L, &e) == 0.5;   // as consts_from_problem decides
-  const int64_t total = run_tiles(n_cand) * k_steps;
-  auto launch = [&](auto pl2_tag) {
-    constexpr bool P = decltype(pl2_tag)::value;
-    k_episode_run<MPC_INTEG_RECT, P><<<run_grid<MPC_INTEG_RECT, P>(total), kRunThreads, 0, st>>>(
-        S, ctl, k_steps, n_cand, n_steps, index_base, rc, rec, out, scratch, *cfg, log,
-        log ? log_capacity : 0, step_clock);
-  };
-  if (pl2)
-    launch(std::true_type{});
-  else
-    launch(std::false_type{});
-  return last_hip_status();
-}
-
-#ifdef MPC_RUN_STATS
-// Debug builds only: the run's phase counters (mpc_run.h), then zeroed.
-int mpc_debug_run_stats(unsigned long long* host32) {
-  if (hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpyFromSymbol(host32, HIP_SYMBOL(g_run_stats), 32 * 8) != hipSuccess)
-    return MPC_ERR_HIP;
-  unsigned long long z[32] = {0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_run_stats), z, sizeof(z)) == hipSuccess ? MPC_OK
-                                                                                : MPC_ERR_HIP;
-}
-// Debug builds only: per-unit timestamps [n_units][8] (n_units <= 1 << 20).
-int mpc_debug_run_unit_times(unsigned long long* host, int64_t n_units) {
-  if (n_units < 0 || n_units > (1 << 20)) return MPC_ERR_ARG;
-  if (hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpyFromSymbol(host, HIP_SYMBOL(g_run_ut), n_units * 8 * 8) != hipSuccess)
-    return MPC_ERR_HIP;
-  return MPC_OK;
-}
-// Debug builds only: the per-step timeline [512][5], then reset (min fields to ~0).
-int mpc_debug_run_timeline(unsigned long long* host2560) {
-  if (hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpyFromSymbol(host2560, HIP_SYMBOL(g_run_tl), 512 * 5 * 8) != hipSuccess)
-    return MPC_ERR_HIP;
-  static unsigned long long z[512][5];
-  for (int j = 0; j < 512; ++j)
-    for (int f = 0; f < 5; ++f) z[j][f] = f == 0 ? ~0ull : 0ull;
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_run_tl), z, sizeof(z)) == hipSuccess ? MPC_OK
-                                                                              : MPC_ERR_HIP;
-}
-#endif
-
 int mpc_episode_chain_error(const void* state, int32_t* error, mpc_stream_t stream) {
   if (!state || !error) return MPC_ERR_ARG;
   uint32_t e = 0;
@@ -801,16 +716,5 @@ int mpc_fulltree_argmin_batched(const mpc_fulltree_problem_t* problems,
   });
   return last_hip_status();
 }
-
-#ifdef MPC_CHAIN_TIMELINE
-// Debug builds only (tools/chain_timeline.py): the last chained launch's
-// per-block ticks, kTlBlocks x 6 uint64 (see mpc_episode.h).
-int mpc_debug_chain_timeline(uint64_t* host) {
-  if (hipDeviceSynchronize() != hipSuccess) return MPC_ERR_HIP;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_chain_tl), sizeof(g_chain_tl)) == hipSuccess
-             ? MPC_OK
-             : MPC_ERR_HIP;
-}
-#endif
 
 }  // extern "C"

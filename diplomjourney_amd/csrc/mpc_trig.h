@@ -59,13 +59,10 @@ constexpr double kT[16] = {0x1.090dd50c4e26cp-18, -0x1.46ffa51d98a1ep-17, 0x1.47
 // (loop-invariant) coefficient into the accumulator first: two VALU ops and
 // two VGPRs per coefficient.  The three-address VOP3 form with the
 // coefficient in an SGPR pair is one VALU op and no VGPRs.
-#ifndef MPC_COEF_REG
-#define MPC_COEF_REG "s"   // where Horner coefficients live: "s" SGPR pair, "v" VGPR pair
-#endif
 MPC_HD inline double fma_k(double a, double b, double c) {
 #if defined(__HIP_DEVICE_COMPILE__)
   double r;
-  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), MPC_COEF_REG(c));
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
   return r;
 #else
   return fma(a, b, c);
@@ -182,9 +179,7 @@ MPC_HD inline double tan_small(double x, const Leads* ld = nullptr) {
 #endif
   r = fma(r, fma(-q, r, 1.0), r);
   double R = p * r;
-#ifndef MPC_TAN_NOCORR
   R = fma(r, fma(-q, R, p), R);           // quotient correction
-#endif
   return fma(x * s, R, x);
 }
 

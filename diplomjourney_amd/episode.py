@@ -411,54 +411,6 @@ class DeviceEpisode:
         self.expand(events, controls)
         self.advance()
 
-    def run(self, batches, clock=None):
-        """len(batches) MPC steps in ONE persistent launch per log_capacity
-        steps (mpc_episode_run; rect+cum, one GPU): step j streams the resident
-        batch batches[j] = (v_sc, beta_sc).  The same steps, bit for bit, as
-        calling step(controls=batches[j]) on a two-launch episode.  clock:
-        optional int64 device tensor [len(batches)] of per-step completion
-        ticks (s_memrealtime, 100 MHz)."""
-        if self.integrator != "rect+cum" or self.exchange:
-            raise ValueError("the persistent run needs integrator rect+cum on one GPU")
-        self.flush()
-        L, st = self.lib, self._stream()
-        if not hasattr(self, "_run_ws"):
-            self._run_ws = torch.zeros(
-                L.mpc_episode_run_workspace_bytes(self.n_local, self.n_steps),
-                dtype=torch.uint8, device=self.v_sc.device)
-            self._tables = {}
-        done, k_all = 0, len(batches)
-        while done < k_all:
-            part = batches[done:done + self.log_capacity]
-            table = self._ptr_table(part)
-            native.check(L.mpc_episode_run(
-                ctypes.byref(self.cfg), self.state.data_ptr(), table.data_ptr(), len(part),
-                self.n_local, self.n_steps, self.lo, self._integ, self._run_ws.data_ptr(),
-                self._run_ws.numel(), self.local.data_ptr(), self.log.data_ptr(),
-                self.log_capacity, clock[done:].data_ptr() if clock is not None else None, st),
-                "mpc_episode_run")
-            self.steps_enqueued += len(part)
-            done += len(part)
-        if batches:
-            self.cur = batches[-1]
-
-    def _ptr_table(self, batches):
-        """Device array of the batches' (v, beta) pointers, built once per
-        distinct list (so a graph-captured run replays a resident table)."""
-        key = tuple((v.data_ptr(), b.data_ptr()) for v, b in batches)
-        t = self._tables.get(key)
-        if t is None:
-            for c in batches:
-                v, b = self._check_controls(c)
-                if v.data_ptr() % 16 or b.data_ptr() % 16 or self.n_local % 2:
-                    raise ValueError("persistent run: 16-B aligned controls, even n_local")
-            t = torch.tensor([p for pair in key for p in pair], dtype=torch.int64,
-                             device=self.v_sc.device)
-            if len(self._tables) > 64:
-                self._tables.clear()
-            self._tables[key] = t
-        return t
-
     def _chainable(self, controls):
         v, b = controls
         return (self.integrator == "rect+cum" and self.n_local % 2 == 0

@@ -31,7 +31,7 @@ EXPORTS = (
     "mpc_sample_controls", "mpc_episode_state_bytes", "mpc_episode_reset",
     "mpc_episode_expand", "mpc_episode_advance", "mpc_episode_sample", "mpc_episode_partials",
     "mpc_episode_finalize", "mpc_episode_rollout", "mpc_episode_step", "mpc_episode_chain_step",
-    "mpc_episode_chain_error", "mpc_episode_run_workspace_bytes", "mpc_episode_run",
+    "mpc_episode_chain_error",
     "mpc_episode_generate_workspace_bytes", "mpc_episode_generate_step",
     "mpc_fulltree_workspace_bytes", "mpc_fulltree_argmin",
     "mpc_fulltree_batched_workspace_bytes", "mpc_fulltree_argmin_batched",
@@ -146,11 +146,6 @@ def lib():
                                          _P, _P, _P, _I32, _P, _I32, _P]
     L.mpc_episode_chain_error.restype = ctypes.c_int
     L.mpc_episode_chain_error.argtypes = [_P, ctypes.POINTER(_I32), _P]
-    L.mpc_episode_run_workspace_bytes.restype = ctypes.c_size_t
-    L.mpc_episode_run_workspace_bytes.argtypes = [_I64, _I32]
-    L.mpc_episode_run.restype = ctypes.c_int
-    L.mpc_episode_run.argtypes = [ctypes.POINTER(MpcEpisodeConfig), _P, _P, _I32, _I64, _I32,
-                                  _I64, _I32, _P, ctypes.c_size_t, _P, _P, _I32, _P, _P]
     L.mpc_episode_generate_workspace_bytes.restype = ctypes.c_size_t
     L.mpc_episode_generate_workspace_bytes.argtypes = [_I64, _I32]
     L.mpc_episode_generate_step.restype = ctypes.c_int

@@ -275,39 +275,9 @@ int mpc_episode_generate_step(const mpc_episode_config_t* cfg, void* state, int6
                               int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
                               size_t ws_bytes, mpc_result_t* out, mpc_episode_log_t* log,
                               int32_t log_capacity, mpc_stream_t stream);
-/* Persistent run (integrator MPC_INTEG_RECT | MPC_HEADING_CUMULATIVE, one GPU):
- * k_steps MPC steps of the device-resident episode in ONE launch — the same
- * steps as k_steps two-launch mpc_episode_step calls (advance non-NULL) on the
- * same controls, bit for bit.  Step j streams the caller-resident controls
- * ctl[2j] (v_sc) / ctl[2j+1] (beta_sc): `ctl` is a DEVICE array of 2*k_steps
- * pointers, each 16-B aligned, [n_steps][n_cand] fp64, n_cand even.  Units of
- * 512 candidates (step, tile) go round-robin to the launch's registered
- * streaming blocks; step j+1's candidates stream while step j is being
- * selected (the kRotCum rollout needs the start pose only for its final
- * transform), and one selecting block reduces step j's unit records, re-rolls
- * the winner and applies the episode update (finishing logic, operator
- * events, restart, log record, next step's constants), publishing step j+1's
- * head in tagged words.  Replaces, for K steps at once, the math_mpc loop
- * body math_model_tree.py:515-635 (as mpc_episode_chain_step does per step).
- *   ws          mpc_episode_run_workspace_bytes(n_cand, n_steps); its polled
- *               part is zeroed on `stream` before the launch
- *   out         the LAST step's winner (re-rolled states)
- *   log         one record per step; log_capacity >= k_steps (MPC_ERR_ARG)
- *   step_clock  optional device array [k_steps]: s_memrealtime (100 MHz) at the
- *               moment step j's successor head was published (the MPC-step
- *               period = consecutive differences)
- * cfg must be the configuration the state was reset with (a wheelbase-form
- * mismatch sets chain error 2); a bounded wait that timed out sets 3. */
-size_t mpc_episode_run_workspace_bytes(int64_t n_cand, int32_t n_steps);
-int mpc_episode_run(const mpc_episode_config_t* cfg, void* state, const double* const* ctl,
-                    int32_t k_steps, int64_t n_cand, int32_t n_steps, int64_t index_base,
-                    int32_t integrator, void* ws, size_t ws_bytes, mpc_result_t* out,
-                    mpc_episode_log_t* log, int32_t log_capacity, uint64_t* step_clock,
-                    mpc_stream_t stream);
-/* Nonzero if a chained step or a persistent run went wrong: 1 = a chained
- * step's wait for the published constants timed out (the launch then ran on
- * stale constants); 2 = cfg's wheelbase form disagreed with the state's;
- * 3 = a persistent run's bounded wait timed out (its results are invalid).
+/* Nonzero if a chained step went wrong: 1 = a chained step's wait for the
+ * published constants timed out (the launch then ran on stale constants);
+ * 2 = cfg's wheelbase form disagreed with the state's.
  * Reads the device state (syncs). */
 int mpc_episode_chain_error(const void* state, int32_t* error, mpc_stream_t stream);
 

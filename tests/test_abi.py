@@ -93,39 +93,6 @@ def test_argument_validation_without_gpu():
                                         fake, None) == abi.MPC_ERR_ARG
 
 
-def test_run_argument_validation_without_gpu():
-    """mpc_episode_run rejects bad arguments before any HIP call: odd or
-    too-large candidate counts, no steps, a log shorter than the run, a
-    non-cumulative integrator, a short workspace."""
-    from diplomjourney_amd.episode import reference_episode_config
-    L = native.lib()
-    cfg = reference_episode_config()
-    fake = ctypes.c_void_p(0x1000)
-    cum = abi.INTEGRATORS["rect+cum"]
-    n, ns = 1000, 10
-    wsb = L.mpc_episode_run_workspace_bytes(n, ns)
-    assert wsb >= 2 * 2 * 4 * 8 + 808
-    assert L.mpc_episode_run_workspace_bytes(1, ns) == 0
-
-    def call(**kw):
-        a = dict(k=4, n=n, ns=ns, base=0, integ=cum, ws=fake, wsb=wsb, out=fake, log=fake,
-                 cap=16)
-        a.update(kw)
-        return L.mpc_episode_run(ctypes.byref(cfg), fake, fake, a["k"], a["n"], a["ns"], a["base"],
-                                 a["integ"], a["ws"], a["wsb"], a["out"], a["log"], a["cap"],
-                                 None, None)
-
-    assert call(k=0) == abi.MPC_ERR_ARG
-    assert call(n=999) == abi.MPC_ERR_ARG
-    assert call(n=2 ** 31) == abi.MPC_ERR_ARG
-    assert call(ns=0) == abi.MPC_ERR_ARG
-    assert call(out=None) == abi.MPC_ERR_ARG
-    assert call(cap=3) == abi.MPC_ERR_ARG          # one log slot per step
-    assert call(base=-1) == abi.MPC_ERR_ARG
-    assert call(integ=abi.INTEGRATORS["rect+rot"]) == abi.MPC_ERR_UNSUPPORTED
-    assert call(wsb=wsb - 1) == abi.MPC_ERR_WORKSPACE
-
-
 def test_no_cpu_fallback(monkeypatch, tmp_path):
     """The product binding raises when the HIP library is absent."""
     monkeypatch.setattr(native, "_lib", None)

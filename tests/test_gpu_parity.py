@@ -586,129 +586,6 @@ def test_chained_exchange_path_and_graph_capture(engine, wheelbase):
             dist.destroy_process_group()
 
 
-# ---------------------------------------------------------------------------
-# Persistent run (mpc_episode_run): K steps in one launch.
-
-def _pool(engine, n, ns, count, seed):
-    from diplomjourney_amd import math_model_tree as mmt
-    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
-    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
-    return [engine.sample_controls(V, B, n, ns, seed + i) for i in range(count)]
-
-
-def _two_launch_log(engine, n, ns, batches, wheelbase=None, cap=512, max_steps=None):
-    from diplomjourney_amd.episode import DeviceEpisode
-    ref = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=cap, L=wheelbase)
-    if max_steps:
-        ref.cfg.max_steps = max_steps
-    for c in batches:
-        ref.step(controls=c)
-    return ref, _episode_log(ref)
-
-
-@pytest.mark.parametrize("wheelbase", [0.5, 0.45])
-def test_run_matches_two_launch_episode(engine, wheelbase):
-    """The persistent run (every step's tiles streamed by one launch, block 0
-    selecting step after step) logs exactly the two-launch rect+cum episode
-    over 160 steps of resident batches — operator events at p = 60/90/110 and
-    an episode restart (step limit 120) included (the restart's t reset is the case where the
-    streaming blocks' speculated step size is wrong and they recompute) — in
-    runs of 70, 1 and 89 steps, with a partial last tile (50_000 = 97 x 512 +
-    336) and both wheelbase forms; the last step's re-rolled winner equals the
-    two-launch finalize's record byte for byte."""
-    from diplomjourney_amd.episode import DeviceEpisode
-    n, ns, steps = 50_000, 10, 160
-    pool = _pool(engine, n, ns, 8, 500)
-    batches = [pool[i % 8] for i in range(steps)]
-    ref, want = _two_launch_log(engine, n, ns, batches, wheelbase, max_steps=120)
-    assert len(want) == steps and {r[8] for r in want} >= {60, 90, 110}
-    assert len({r[9] for r in want}) >= 2, "no episode restart exercised"
-    ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=512, L=wheelbase)
-    ep.cfg.max_steps = 120
-    ep.run(batches[:70])
-    ep.run(batches[70:71])
-    ep.run(batches[71:])
-    assert _episode_log(ep) == want
-    assert ep.chain_error() == 0
-    assert bytes(ep.local.cpu().numpy()) == bytes(ref.local.cpu().numpy())
-
-
-def test_run_blocks_many_steps_ahead(engine):
-    """Few tiles per step (4096 candidates = 8 units) and a full-size grid:
-    streaming blocks claim units up to ~100 steps ahead of the selection,
-    speculate the step size over several steps and wait for the published
-    heads; the log equals the two-launch episode.  The per-step completion
-    clock is monotonic."""
-    from diplomjourney_amd.episode import DeviceEpisode
-    n, ns, steps = 4096, 6, 300
-    pool = _pool(engine, n, ns, 5, 60)
-    batches = [pool[i % 5] for i in range(steps)]
-    _, want = _two_launch_log(engine, n, ns, batches, max_steps=70)
-    assert len({r[9] for r in want}) >= 3
-    ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=512)
-    ep.cfg.max_steps = 70
-    clock = torch.zeros(steps, dtype=torch.int64, device="cuda")
-    ep.run(batches, clock=clock)
-    assert _episode_log(ep) == want
-    assert ep.chain_error() == 0
-    c = clock.cpu()
-    assert bool((c[1:] >= c[:-1]).all()) and int(c[0]) > 0
-
-
-def test_run_graph_capture_and_replay(engine):
-    """A run captured in a HIP graph (memset node + launch) replays twice and
-    continues the episode: 2 x 40 steps equal 80 two-launch steps."""
-    from diplomjourney_amd.episode import DeviceEpisode
-    n, ns, k = 30_000, 10, 40
-    pool = _pool(engine, n, ns, 4, 300)
-    batches = [pool[i % 4] for i in range(k)]
-    _, want = _two_launch_log(engine, n, ns, batches + batches)
-    ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=128)
-    ep.run(batches[:1])                      # allocates the workspace and table cache
-    ep.reset()
-    ep._ptr_table(batches)                   # table resident before capture
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        ep.run(batches)
-    ep.steps_enqueued = 0
-    g.replay()
-    g.replay()
-    ep.steps_enqueued = 2 * k
-    assert _episode_log(ep) == want
-    assert ep.chain_error() == 0
-
-
-def test_run_wheelbase_mismatch_is_flagged(engine):
-    """A run whose cfg wheelbase form differs from the state's constants sets
-    chain error 2."""
-    from diplomjourney_amd.episode import DeviceEpisode
-    n, ns = 20_000, 10
-    pool = _pool(engine, n, ns, 2, 40)
-    ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=16)
-    ep.run(pool)
-    assert ep.chain_error() == 0
-    ep.cfg.L = 0.45                          # state reset with L = 0.5
-    ep.run(pool)
-    assert ep.chain_error() == 2
-
-
-def test_run_two_units_per_block_and_step(engine):
-    """More units per step than streaming blocks (1.1e6 candidates = 2149
-    units over ~1000 blocks): a block holds two units of the same step, both
-    can be unselected when the second one's loop ends (the parked one is then
-    waited for, not overwritten).  Equals the two-launch episode."""
-    from diplomjourney_amd.episode import DeviceEpisode
-    n, ns, steps = 1_100_000, 6, 14
-    pool = _pool(engine, n, ns, 7, 800)
-    batches = [pool[i % 7] for i in range(steps)]
-    _, want = _two_launch_log(engine, n, ns, batches)
-    ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64)
-    ep.run(batches)
-    assert _episode_log(ep) == want
-    assert ep.chain_error() == 0
-
-
 @pytest.mark.parametrize("extra", [[], ["--integrator", "rect+rot"]])
 def test_bench_contract(extra):
     """bench.py (a short run, no CPU leg) prints ONE JSON line with the
@@ -802,12 +679,29 @@ def test_generated_step_arguments(engine):
     assert call(ratio=100.0) == abi.MPC_OK
 
 
+def _pool(engine, n, ns, count, seed):
+    from diplomjourney_amd import math_model_tree as mmt
+    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
+    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
+    return [engine.sample_controls(V, B, n, ns, seed + i) for i in range(count)]
+
+
+def _two_launch_log(engine, n, ns, batches, wheelbase=None, cap=512, max_steps=None):
+    from diplomjourney_amd.episode import DeviceEpisode
+    ref = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=cap, L=wheelbase)
+    if max_steps:
+        ref.cfg.max_steps = max_steps
+    for c in batches:
+        ref.step(controls=c)
+    return ref, _episode_log(ref)
+
+
 @pytest.mark.parametrize("ns", [2, 3, 12])
-def test_short_and_long_horizons_chain_and_run(engine, ns):
+def test_short_and_long_horizons_chain(engine, ns):
     """Horizons around the head prefetch three steps before a loop's end
     (none for N = 2, at the first step for N = 3) and the config-D length
-    N = 12: the chained steps and the persistent run log exactly the
-    two-launch rect+cum episode over 60 steps with a restart."""
+    N = 12: the chained steps log exactly the two-launch rect+cum episode
+    over 60 steps with a restart."""
     from diplomjourney_amd.episode import DeviceEpisode
     n, steps = 20_000, 60
     pool = _pool(engine, n, ns, 4, 900 + ns)
@@ -816,12 +710,9 @@ def test_short_and_long_horizons_chain_and_run(engine, ns):
     assert len({r[9] for r in want}) >= 2, "no episode restart exercised"
     ch = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=512, chain=True)
     ch.cfg.max_steps = 40
+    ch.reset()
     for c in batches:
         ch.step(controls=c)
     ch.flush()
     assert _episode_log(ch) == want
-    run = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=512)
-    run.cfg.max_steps = 40
-    run.run(batches)
-    assert _episode_log(run) == want
-    assert run.chain_error() == 0 and ch.chain_error() == 0
+    assert ch.chain_error() == 0

@@ -139,7 +139,7 @@ def test_candidate_enumeration_order():
 def test_bench_defaults(monkeypatch):
     """bench.py's defaults: config C on one GPU, the chained rect+cum step for
     the episode workloads (B, C, D), rect+rot for E/F/G, 500 timed steps for
-    the ~40-us workloads; the persistent run needs rect+cum."""
+    the ~40-us workloads."""
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -152,7 +152,7 @@ def test_bench_defaults(monkeypatch):
     a = parse()
     assert (a.workload, a.gpus, a.steps, a.warmup, a.integrator, a.inputs) == (
         "C", 1, 500, 20, "rect+cum", "resident")
-    assert not a.no_chain and not a.run
+    assert not a.no_chain
     assert parse("--workload", "D").integrator == "rect+cum"
     assert parse("--workload", "B").integrator == "rect+cum"
     assert parse("--workload", "E").integrator == "rect+rot"
