@@ -70,15 +70,21 @@ class MpcEpisodeConfig(ctypes.Structure):
         "start_x", "start_y", "start_phi", "start_v", "start_beta", "target_x", "target_y",
         "L", "delta_t", "eps", "v_max", "v_min", "delta_v", "ratio_v", "delta_beta",
         "ratio_beta", "beta_bound", "radius_u_turn", "turn_distance", "event_target_x",
-        "event_target_y")] + [(n, ctypes.c_int32) for n in (
+        "event_target_y", "incumbent0")] + [(n, ctypes.c_int32) for n in (
         "p_turn_right", "p_turn_left", "p_new_target", "slow_new_target", "slow_turn",
-        "max_steps")] + [("seed", ctypes.c_uint64)]
+        "max_steps", "enumerate", "reserved_")] + [("seed", ctypes.c_uint64)]
+
+
+# mpc_episode_log_t.status bits (include/mpc_rollout.h)
+MPC_EP_STALE, MPC_EP_STUCK, MPC_EP_BREAK, MPC_EP_EVENT, MPC_EP_ARRIVED, MPC_EP_LIMIT = (
+    1, 2, 4, 8, 16, 32)
 
 
 class MpcEpisodeLog(ctypes.Structure):
     """mpc_episode_log_t: one MPC step of the device-resident episode."""
     _fields_ = [("step", ctypes.c_int64), ("index", ctypes.c_int64), ("p", ctypes.c_int32),
-                ("episode", ctypes.c_int32)] + [(n, ctypes.c_double) for n in (
+                ("episode", ctypes.c_int32), ("found", ctypes.c_int32),
+                ("status", ctypes.c_int32)] + [(n, ctypes.c_double) for n in (
                     "cost", "x", "y", "phi", "v", "beta")]
 
 

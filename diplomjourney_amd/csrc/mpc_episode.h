@@ -27,8 +27,11 @@ constexpr int kPubWords = kConstsWords + 2;   // Consts, then t
 static_assert(sizeof(Consts) % 4 == 0 && kPubWords <= 64, "published words: one wave");
 
 // EpisodeHead (mpc_kernels.h): the scalars; the grids only feed the sampler.
+// The stale trajectory follows the head (staged and stored with it as one
+// run of kStagedWords words).
 struct EpisodeState {
   EpisodeHead h;
+  StaleTraj st;        // right after the head: staged and stored with it
   double grid_v[kEpMaxGrid];
   double grid_b[kEpMaxGrid];
   uint32_t done;       // blocks of the running fused launch that have finished
@@ -39,6 +42,7 @@ struct EpisodeState {
   // says whether its value is this step's.  Tag 0: none.
   alignas(128) uint64_t chain_pub[kPubWords];
 };
+static_assert(offsetof(EpisodeState, st) == sizeof(EpisodeHead), "stale trajectory follows the head");
 
 __device__ inline Consts episode_consts(const EpisodeHead& S, double x, double y, double phi,
                                         double L, double t_a, double t_b) {
@@ -57,8 +61,12 @@ __device__ inline Consts episode_consts(const EpisodeHead& S, double x, double y
 }
 
 // Episode.reset() / math_mpc's prologue (:521-541): start pose, target, line
-// origin at the start, t = 0, p = 1, m = 0, incumbent = control_criterion of
-// the line origin (the reference's first optimal_criterion, :676).
+// origin at the start, t = 0, p = 1, m = 0 (the script resets m between its
+// two runs, :737), recursive = False;
+// incumbent = cfg.incumbent0, or control_criterion of the line origin with
+// the episode's target (the reference's first optimal_criterion is that of
+// config.py's target, :676).  optimal_trajectory / result_v / result_beta
+// are module globals the reference never resets: they carry over.
 __device__ inline void episode_restart(const mpc_episode_config_t& c, EpisodeHead& S) {
   S.x = c.start_x;
   S.y = c.start_y;
@@ -74,8 +82,13 @@ __device__ inline void episode_restart(const mpc_episode_config_t& c, EpisodeHea
   S.m = 0;
   S.steps_for_slowing = 0;
   S.episodes += 1;
-  const Consts K0 = episode_consts(S, S.x_0, S.y_0, 0.0, c.L, 0.0, c.delta_t);
-  S.incumbent = cost(S.x_0, S.y_0, K0);
+  S.recursive = 0;
+  if (c.incumbent0 != 0.0) {
+    S.incumbent = c.incumbent0;
+  } else {
+    const Consts K0 = episode_consts(S, S.x_0, S.y_0, 0.0, c.L, 0.0, c.delta_t);
+    S.incumbent = cost(S.x_0, S.y_0, K0);
+  }
 }
 
 __device__ __forceinline__ uint64_t episode_seed(const mpc_episode_config_t& c,
@@ -173,8 +186,9 @@ __global__ __launch_bounds__(kBlock) void k_episode_sample(
     for (int i = 0; i < nv; ++i) S->grid_v[i] = s_v[i];
     for (int i = 0; i < nb; ++i) S->grid_b[i] = s_b[i];
   }
-  if (n_grid == 0) return;
-  sample_items(s_grid, n_grid, n_cand, n_steps, seed, base, 1, v, b, n_cand, pairs);
+  if (n_grid == 0 && !c.enumerate) return;
+  sample_items(s_grid, n_grid, n_cand, n_steps, seed, base, c.enumerate ? 2 : 1, v, b, n_cand,
+               pairs);
 }
 
 // ---------------------------------------------------------------------------
@@ -336,13 +350,21 @@ __device__ __forceinline__ double tr_at(const Winner& r, int k, int q) {
   return k == 0 ? a : (k == 1 ? b : c);
 }
 
-// Episode._advance: finishing logic (:392-414), events (:564-569), restart.
+// Episode._advance = the rest of math_mpc's loop body after predictive_control
+// (:542-574 with :351-429): the returned pose is the winner's layer state
+// picked by the finishing logic (:392-414) — or, when no candidate beat the
+// incumbent, the STALE optimal_trajectory / result_v / result_beta of the
+// last improving step (the globals :351-359 did not touch), with the same
+// finishing logic; then the stuck detector (:559-563: a pose equal to the
+// previous one sets `recursive`, the next step with it set ends the episode
+// before the events), the operator events (:564-569), p += 1, and the loop
+// condition (:542: on target ends the episode).  An ended episode restarts
+// (the bench's episode stream; the reference's loop returns).
 // Operates on a register copy of the episode scalars (the caller loads it
-// once and stores it back once).
-// The step's log record is filled in `L` (LDS); the caller stores it
-// (log_slot) together with the head.
+// once and stores it back once).  The step's log record is filled in `L`
+// (LDS); the caller stores it (log_slot) together with the head.
 __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeHead& H,
-                                       const Winner& r, mpc_episode_log_t& L) {
+                                       StaleTraj& st, const Winner& r, mpc_episode_log_t& L) {
   EpisodeHead* S = &H;
   S->steps_for_slowing -= 1;
   S->incumbent = 9223372036854775808.0;  // float(sys.maxsize), :428
@@ -350,27 +372,58 @@ __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeHea
   L.index = r.found ? r.index : -1;
   L.p = S->p;
   L.episode = S->episodes;
+  L.found = r.found;
   L.cost = r.cost;
+  int32_t status = 0;
   S->step += 1;
-  if (r.found) {
+  if (r.found) {   // :352-359: the globals take the winner
     const int last = r.n_steps - 1;
-    const int probe = last < 2 ? last : 2;
-    int k = 0;
-    if (S->m == 2) {
-      k = 2;
-    } else if (S->m == 1) {
-      k = 1;
-      S->m += 1;
-    } else {
-      const double ex = S->x_t - tr_at(r, probe, 0), ey = S->y_t - tr_at(r, probe, 1);
-      if (ex * ex + ey * ey <= c.eps) S->m += 1;
+    for (int k = 0; k < 3; ++k)
+      for (int q = 0; q < 3; ++q) st.ot[k][q] = tr_at(r, k < last ? k : last, q);
+    st.v = r.v;
+    st.beta = r.beta;
+    S->has_traj = 1;
+  } else {
+    status |= MPC_EP_STALE;
+    if (!S->has_traj) {
+      // the reference's initial optimal_trajectory [[[0]]] has no layer
+      // states (it would raise IndexError): stay at the pose
+      for (int k = 0; k < 3; ++k) {
+        st.ot[k][0] = S->x;
+        st.ot[k][1] = S->y;
+        st.ot[k][2] = S->phi;
+      }
+      st.v = S->v;
+      st.beta = S->beta;
     }
-    k = k < last ? k : last;
-    S->x = tr_at(r, k, 0);
-    S->y = tr_at(r, k, 1);
-    S->phi = tr_at(r, k, 2);
-    S->v = r.v;
-    S->beta = r.beta;
+  }
+  // finishing logic on optimal_trajectory[0] (:388-414): probe layer 2 (the
+  // last layer for horizons < 3), return layer k
+  int k = 0;
+  if (S->m == 2) {
+    k = 2;
+  } else if (S->m == 1) {
+    k = 1;
+    S->m += 1;
+  } else {
+    const double ex = S->x_t - st.ot[2][0], ey = S->y_t - st.ot[2][1];
+    if (ex * ex + ey * ey <= c.eps) S->m += 1;
+  }
+  const double x_prev = S->x, y_prev = S->y;   // x_previous / y_previous (:570-571)
+  S->x = st.ot[k][0];   // (st lives in LDS: a dynamic index is an LDS address)
+  S->y = st.ot[k][1];
+  S->phi = st.ot[k][2];
+  S->v = st.v;
+  S->beta = st.beta;
+  bool ended = false;
+  if (S->recursive) {            // :559-561 "Recursive error." -> break
+    status |= MPC_EP_BREAK;
+    ended = true;
+  } else {
+    if (S->x == x_prev && S->y == y_prev) {   // :562-563
+      S->recursive = 1;
+      status |= MPC_EP_STUCK;
+    }
     double tx, ty;
     if (S->p == c.p_turn_right) {
       turn_target(S->x, S->y, S->phi, c.turn_distance, c.radius_u_turn, -1.0, tx, ty);
@@ -379,6 +432,7 @@ __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeHea
       S->x_0 = S->x;
       S->y_0 = S->y;
       S->steps_for_slowing = c.slow_turn;
+      status |= MPC_EP_EVENT;
     }
     if (S->p == c.p_turn_left) {
       turn_target(S->x, S->y, S->phi, c.turn_distance, c.radius_u_turn, +1.0, tx, ty);
@@ -387,6 +441,7 @@ __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeHea
       S->x_0 = S->x;
       S->y_0 = S->y;
       S->steps_for_slowing = c.slow_turn;
+      status |= MPC_EP_EVENT;
     }
     if (S->p == c.p_new_target) {
       S->x_t = c.event_target_x;
@@ -394,24 +449,33 @@ __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeHea
       S->x_0 = S->x;
       S->y_0 = S->y;
       S->steps_for_slowing = c.slow_new_target;
+      status |= MPC_EP_EVENT;
     }
     S->p += 1;
     const double ex = S->x_t - S->x, ey = S->y_t - S->y;
-    if (ex * ex + ey * ey <= c.eps || S->p > c.max_steps) episode_restart(c, *S);
+    if (ex * ex + ey * ey <= c.eps) {                   // :542
+      status |= MPC_EP_ARRIVED;
+      ended = true;
+    } else if (c.max_steps > 0 && S->p > c.max_steps) {
+      status |= MPC_EP_LIMIT;
+      ended = true;
+    }
   }
-  episode_prepare(c, *S);
   L.x = S->x;
   L.y = S->y;
   L.phi = S->phi;
   L.v = S->v;
   L.beta = S->beta;
+  L.status = status;
+  if (ended) episode_restart(c, *S);
+  episode_prepare(c, *S);
 }
 
 __device__ void episode_hook(const mpc_episode_config_t& c, const EpisodeHook& h,
-                             const Winner& r, EpisodeHead& H, mpc_episode_log_t& L,
-                             mpc_episode_log_t*& slot) {
+                             const Winner& r, EpisodeHead& H, StaleTraj& st,
+                             mpc_episode_log_t& L, mpc_episode_log_t*& slot) {
   slot = log_slot(h.log, h.cap, H.step);
-  episode_advance(c, H, r, L);
+  episode_advance(c, H, st, r, L);
 }
 
 // Multi-GPU: lexicographic (cost, global index) selection over the gathered
@@ -423,9 +487,12 @@ __device__ inline void advance_from_results(const mpc_episode_config_t& c, Episo
                                             const mpc_result_t* __restrict__ res, int n,
                                             mpc_episode_log_t* __restrict__ log, int cap,
                                             bool end_chain = true) {
-  __shared__ uint64_t s_head[kHeadWords];
+  __shared__ uint64_t s_head[kStagedWords];
   __shared__ mpc_episode_log_t s_log;
   __shared__ mpc_episode_log_t* s_slot;
+  if (threadIdx.x < kStaleWords)   // the stale trajectory, staged beside the head
+    s_head[kHeadWords + threadIdx.x] = reinterpret_cast<const uint64_t*>(&S->st)[threadIdx.x];
+  __syncthreads();
   if (threadIdx.x == 0) {
     EpisodeHead H = S->h;
     uint64_t bk;
@@ -441,7 +508,7 @@ __device__ inline void advance_from_results(const mpc_episode_config_t& c, Episo
     for (int k = 0; k < 3; ++k)
       for (int q = 0; q < 3; ++q) w.tr[k][q] = r.traj[k < r.n_steps ? k : 0][q];
     s_slot = log_slot(log, cap, H.step);
-    episode_advance(c, H, w, s_log);
+    episode_advance(c, H, *reinterpret_cast<StaleTraj*>(&s_head[kHeadWords]), w, s_log);
     __builtin_memcpy(s_head, &H, sizeof(EpisodeHead));
   }
   __syncthreads();

@@ -616,6 +616,21 @@ struct EpisodeHead {
   int64_t step;
   int32_t p, m, steps_for_slowing, episodes;
   int32_t nv, nb;
+  // math_mpc's stuck detector (:559-563); x_previous / y_previous (:540-541,
+  // :570-571) are always the pose the step starts from, (x, y) above
+  int32_t recursive;
+  int32_t has_traj;    // optimal_trajectory holds a winner (not the initial [[[0]]])
+};
+
+// The module globals optimal_trajectory[0] (layer states 0..2), result_v,
+// result_beta: what a step in which no candidate beats the incumbent returns
+// (stale: :351-359 not taken; the post-processing :366-429 as usual).  Stored
+// right after the head in HBM and staged with it in LDS; the update reads and
+// writes it there (a register copy of head + trajectory would not fit
+// thread 0's registers and lands in scratch).
+struct StaleTraj {
+  double ot[3][3];
+  double v, beta;
 };
 
 struct EpisodeHook {  // single-GPU episode: finalize also advances it
@@ -626,6 +641,9 @@ struct EpisodeHook {  // single-GPU episode: finalize also advances it
   int chain_pub_words = 0;
 };
 constexpr int kHeadWords = static_cast<int>(sizeof(EpisodeHead) / 8);
+constexpr int kStaleWords = static_cast<int>(sizeof(StaleTraj) / 8);
+constexpr int kStagedWords = kHeadWords + kStaleWords;   // head + stale trajectory
+static_assert(kStagedWords <= 64, "staged head: one word per lane");
 constexpr int kLogWords = static_cast<int>(sizeof(mpc_episode_log_t) / 8);
 static_assert(sizeof(EpisodeHead) % 8 == 0 && kHeadWords <= 64, "head: one word per lane");
 static_assert(sizeof(mpc_episode_log_t) % 8 == 0 && kLogWords <= 64, "log: one word per lane");
@@ -642,14 +660,14 @@ __device__ __forceinline__ void store_update(EpisodeHead* H, const uint64_t* s_h
                                              mpc_episode_log_t* slot, const uint64_t* s_log,
                                              uint64_t* chain_pub, int chain_words) {
   const int q = threadIdx.x;
-  if (q < kHeadWords) reinterpret_cast<uint64_t*>(H)[q] = s_head[q];
+  if (q < kStagedWords) reinterpret_cast<uint64_t*>(H)[q] = s_head[q];   // head, then StaleTraj
   if (slot && q < kLogWords) reinterpret_cast<uint64_t*>(slot)[q] = s_log[q];
   if (chain_pub && q < chain_words) chain_pub[q] = 0ull;
 }
 
 __device__ void episode_hook(const mpc_episode_config_t& c, const EpisodeHook& h,
-                             const Winner& r, EpisodeHead& H, mpc_episode_log_t& L,
-                             mpc_episode_log_t*& slot);
+                             const Winner& r, EpisodeHead& H, StaleTraj& st,
+                             mpc_episode_log_t& L, mpc_episode_log_t*& slot);
 
 // Block-record reduction + winner re-roll (+ episode update), run by every
 // thread of one block of NT threads.  SC1: the records were written by
@@ -692,7 +710,7 @@ __device__ __forceinline__ void finalize_block(
   // serialised three scalar round trips in front of wave 0's record loads.)
   static_assert(NT >= 128, "head staging by wave 1");
   static_assert(MPC_MAX_STEPS * 3 <= NT, "trajectory stored one value per lane");
-  __shared__ uint64_t s_head[kHeadWords];
+  __shared__ uint64_t s_head[kStagedWords];
   __shared__ mpc_episode_log_t s_log;   // filled field by field by the update
   __shared__ mpc_episode_log_t* s_slot;
   __shared__ uint64_t s_key[NT / 64];
@@ -735,7 +753,7 @@ __device__ __forceinline__ void finalize_block(
         i = r[q].idx;
       }
   }
-  if (KDEV && hook.H && threadIdx.x >= 64 && threadIdx.x < 64 + kHeadWords)
+  if (KDEV && hook.H && threadIdx.x >= 64 && threadIdx.x < 64 + kStagedWords)
     s_head[threadIdx.x - 64] = reinterpret_cast<const uint64_t*>(hook.H)[threadIdx.x - 64];
   wave_argmin(k, i);
   // Each wave's best candidate's controls, loaded while the waves' minima are
@@ -787,7 +805,8 @@ __device__ __forceinline__ void finalize_block(
     if (threadIdx.x == 0) {   // emit_winner ended with a barrier
       EpisodeHead H;
       __builtin_memcpy(&H, s_head, sizeof(EpisodeHead));
-      episode_hook(ecfg, hook, w, H, s_log, s_slot);
+      episode_hook(ecfg, hook, w, H, *reinterpret_cast<StaleTraj*>(&s_head[kHeadWords]), s_log,
+                   s_slot);
       __builtin_memcpy(s_head, &H, sizeof(EpisodeHead));
     }
     __syncthreads();
@@ -1040,6 +1059,8 @@ constexpr int kSampleLdsEntries = 2048;  // expanded (v, beta) grid staged in LD
 // grid |V| x |B| (<= 451 entries for the reference's acceleration limits) is
 // expanded once per block into LDS, so the per-element lookup is one
 // ds_read_b128 instead of a division by |B| and two loads.
+// cprefix 2 (the episode's enumeration mode): candidates past the grid are
+// padding — NaN controls, a NaN cost, never chosen.
 __device__ void sample_items(const double2* s_grid, uint32_t n_grid, int64_t n_cand, int n_steps,
                              uint64_t seed, int64_t base, int cprefix, double* __restrict__ v,
                              double* __restrict__ b, int64_t ld, int pairs) {
@@ -1049,10 +1070,14 @@ __device__ void sample_items(const double2* s_grid, uint32_t n_grid, int64_t n_c
        it += static_cast<int64_t>(gridDim.x) * kBlock) {
     const int64_t c = it * cpt;
     const uint64_t g = static_cast<uint64_t>(base + c);
+    const double2 pad = make_double2(__builtin_nan(""), 0.0);
     for (int st = 0; st < n_steps; ++st) {
-      const double2 e0 = s_grid[grid_entry(seed, st, g, n_grid, cprefix)];
+      const double2 e0 =
+          (cprefix == 2 && g >= n_grid) ? pad : s_grid[grid_entry(seed, st, g, n_grid, cprefix)];
       if (pairs) {
-        const double2 e1 = s_grid[grid_entry(seed, st, g + 1, n_grid, cprefix)];
+        const double2 e1 = (cprefix == 2 && g + 1 >= n_grid)
+                               ? pad
+                               : s_grid[grid_entry(seed, st, g + 1, n_grid, cprefix)];
         *reinterpret_cast<double2*>(v + st * ld + c) = make_double2(e0.x, e1.x);
         *reinterpret_cast<double2*>(b + st * ld + c) = make_double2(e0.y, e1.y);
       } else {

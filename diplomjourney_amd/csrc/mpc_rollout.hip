@@ -192,7 +192,7 @@ void launch_finalize(hipStream_t st, int32_t integrator, const Rec* part, int n_
 int check_episode_cfg(const mpc_episode_config_t* c) {
   if (!c) return MPC_ERR_ARG;
   if (!(c->ratio_v >= 0) || !(c->ratio_beta >= 0) || c->ratio_v > 1000 || c->ratio_beta > 1000 ||
-      c->max_steps < 1 || !(c->delta_t > 0))
+      c->max_steps < 0 || !(c->delta_t > 0) || (c->enumerate != 0 && c->enumerate != 1))
     return MPC_ERR_ARG;
   return MPC_OK;
 }
@@ -406,7 +406,7 @@ int mpc_episode_generate_step(const mpc_episode_config_t* cfg, void* state, int6
       n_steps > MPC_MAX_STEPS || index_base < 0 || log_capacity < 0)
     return MPC_ERR_ARG;
   if (n_cand < 2 || n_cand % 2 != 0) return MPC_ERR_ARG;   // two candidates per lane
-  if (mode_ok(integrator) != MPC_OK) return MPC_ERR_UNSUPPORTED;
+  if (mode_ok(integrator) != MPC_OK || cfg->enumerate) return MPC_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < mpc_episode_generate_workspace_bytes(n_cand, n_steps))
     return MPC_ERR_WORKSPACE;
   // the expanded grid in LDS: at most (1 + 2 ratio_v) x (1 + 2 ratio_beta) entries

@@ -10,9 +10,12 @@ Per MPC step (one `Episode.step()`):
   3. device: k_rollout_argmin (the HBM-streaming kernel) + k_finalize
   4. multi-GPU: all_gather of the 808-B winner records + k_select_winner
   5. one 808-B device->host read; host applies the reference's finishing
-     logic (:366-429) and operator events (p = 60 / 90 / 110, :564-569)
+     logic (:366-429) — on the stale optimal_trajectory when no candidate
+     beat the incumbent — the stuck detector (:559-563) and the operator
+     events (p = 60 / 90 / 110, :564-569)
 The incumbent is sys.maxsize after the first call, as in the reference
-(:428); the episode restarts from the start pose when the target is reached.
+(:428); an episode that ends (on target, :542, or "Recursive error",
+:559-561) restarts from the start pose.
 """
 import ctypes
 import math
@@ -22,15 +25,24 @@ import time
 import torch
 
 from . import math_model_tree as mmt
-from .abi import LOG_BYTES, RESULT_BYTES, MpcEpisodeConfig, MpcEpisodeLog, make_problem
+from .abi import (LOG_BYTES, MPC_EP_ARRIVED, MPC_EP_BREAK, MPC_EP_EVENT, MPC_EP_LIMIT,
+                  MPC_EP_STALE, MPC_EP_STUCK, RESULT_BYTES, MpcEpisodeConfig, MpcEpisodeLog,
+                  make_problem)
 from .distributed import exchange_winner, gather_results, shard_range
 from . import native
 
 
 class Episode:
     def __init__(self, engine, n_cand_total, n_steps, rank=0, world=1, seed=20261015,
-                 integrator="rect", group=None, start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3)):
+                 integrator="rect", group=None, start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3),
+                 max_steps=0):
         self.eng = engine
+        self.max_steps = int(max_steps)
+        # module globals of the reference that outlive an episode: the last
+        # winner's layer states, result_v, result_beta (None: the initial
+        # [[[0]]], which has no layer states)
+        self.ot = None
+        self.last_log = None
         self.n_total = int(n_cand_total)
         self.n_steps = int(n_steps)
         self.rank, self.world, self.group = rank, world, group
@@ -60,6 +72,8 @@ class Episode:
         self.m = 0
         self.steps_for_slowing = 0
         self.episodes = getattr(self, "episodes", 0) + 1
+        self.x_prev, self.y_prev = x, y
+        self.recursive = False
         self.incumbent = self._criterion0()
 
     def _criterion0(self):
@@ -112,33 +126,59 @@ class Episode:
         return res
 
     def _advance(self, res):
-        """Reference post-processing + episode bookkeeping (:351-429, :542-579)."""
+        """The rest of math_mpc's loop body (:542-574 with :351-429); the same
+        update as the device's episode_advance (csrc/mpc_episode.h)."""
         self.steps_for_slowing -= 1
         self.incumbent = float(sys.maxsize)
-        if not res.found:
-            # nothing beat the incumbent: keep the pose (stale trajectory)
-            return
-        traj = res.trajectory()
+        step_p, status = self.p, 0
+        if res.found:
+            traj = res.trajectory()
+            last = self.n_steps - 1
+            self.ot = [list(traj[min(k, last)]) for k in range(3)]
+            self.ot_v, self.ot_beta = res.v, res.beta
+        else:
+            status |= MPC_EP_STALE
+            if self.ot is None:           # [[[0]]] has no layers: stay at the pose
+                self.ot = [[self.x, self.y, self.phi] for _ in range(3)]
+                self.ot_v, self.ot_beta = self.v, self.beta
         k = 0
         if self.m == 2:
             k = 2
         elif self.m == 1:
             k = 1
             self.m += 1
-        elif mmt.is_on_target(traj[min(2, self.n_steps - 1)][0],
-                              traj[min(2, self.n_steps - 1)][1], self.x_t, self.y_t)[0]:
+        elif mmt.is_on_target(self.ot[2][0], self.ot[2][1], self.x_t, self.y_t)[0]:
             self.m += 1
-        k = min(k, self.n_steps - 1)
-        self.x, self.y, self.phi = traj[k]
-        self.v, self.beta = res.v, res.beta
-        if self.p == 60:
-            self._turn(-1)
-        if self.p == 90:
-            self._turn(+1)
-        if self.p == 110:
-            self._new_target(2, 3)
-        self.p += 1
-        if mmt.is_on_target(self.x, self.y, self.x_t, self.y_t)[0] or self.p > 400:
+        self.x, self.y, self.phi = self.ot[k]
+        self.v, self.beta = self.ot_v, self.ot_beta
+        ended = False
+        if self.recursive:                # "Recursive error." (:559-561)
+            status |= MPC_EP_BREAK
+            ended = True
+        else:
+            if self.x == self.x_prev and self.y == self.y_prev:
+                self.recursive = True
+                status |= MPC_EP_STUCK
+            if self.p == 60:
+                self._turn(-1)
+                status |= MPC_EP_EVENT
+            if self.p == 90:
+                self._turn(+1)
+                status |= MPC_EP_EVENT
+            if self.p == 110:
+                self._new_target(2, 3)
+                status |= MPC_EP_EVENT
+            self.x_prev, self.y_prev = self.x, self.y
+            self.p += 1
+            if mmt.is_on_target(self.x, self.y, self.x_t, self.y_t)[0]:
+                status |= MPC_EP_ARRIVED
+                ended = True
+            elif self.max_steps > 0 and self.p > self.max_steps:
+                status |= MPC_EP_LIMIT
+                ended = True
+        self.last_log = (res.index if res.found else -1, res.cost, step_p, self.x, self.y,
+                         self.phi, self.v, self.beta, int(bool(res.found)), status)
+        if ended:
             self.reset()
 
     def _new_target(self, tx, ty):
@@ -153,10 +193,15 @@ class Episode:
 
 
 def reference_episode_config(start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3), seed=20261015,
-                             max_steps=400):
+                             max_steps=0, incumbent0=0.0, enumerate=False):
     """mpc_episode_config_t with the reference's constants and expressions
     (config.py; grid ratios as math_model_tree.py:241-253 computes them; the
-    operator schedule of :564-569; slow_down bands of :219-226)."""
+    operator schedule of :564-569; slow_down bands of :219-226).  max_steps 0:
+    no step limit (the reference's loop runs until on target or stuck);
+    incumbent0 0: the first incumbent from the episode's target (the
+    reference's, 10000050990.195135, is config.py's target's, :676);
+    enumerate: sampled steps hold exactly the step's |V|*|B| constant
+    sequences (the reference's candidate set), the rest padding."""
     c = mmt._cfg
     return MpcEpisodeConfig(
         start_x=start[0], start_y=start[1], start_phi=start[2], start_v=start[3],
@@ -167,7 +212,7 @@ def reference_episode_config(start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3), see
         beta_bound=c.beta_max + math.radians(c.eps_beta), radius_u_turn=mmt.radius_u_turn,
         turn_distance=2.0, event_target_x=2.0, event_target_y=3.0,
         p_turn_right=60, p_turn_left=90, p_new_target=110, slow_new_target=10, slow_turn=20,
-        max_steps=max_steps, seed=seed)
+        max_steps=max_steps, incumbent0=incumbent0, enumerate=int(bool(enumerate)), seed=seed)
 
 
 class DeviceEpisode:
@@ -179,7 +224,7 @@ class DeviceEpisode:
     def __init__(self, engine, n_cand_total, n_steps, rank=0, world=1, seed=20261015,
                  integrator="rect", group=None, start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3),
                  log_capacity=4096, split=True, exchange=None, chain=False, L=None,
-                 generate=False):
+                 generate=False, max_steps=0, incumbent0=0.0, enumerate=False):
         self.eng = engine
         self.lib = native.lib()
         self.n_total = int(n_cand_total)
@@ -188,7 +233,8 @@ class DeviceEpisode:
         self.lo, self.hi = shard_range(self.n_total, rank, world)
         self.n_local = self.hi - self.lo
         self.integrator = integrator
-        self.cfg = reference_episode_config(start, target, seed)
+        self.cfg = reference_episode_config(start, target, seed, max_steps=max_steps,
+                                            incumbent0=incumbent0, enumerate=enumerate)
         if L is not None:                 # wheelbase other than config.py's (tests: L not 2^k)
             self.cfg.L = float(L)
         dev = engine.device

@@ -181,16 +181,38 @@ typedef struct mpc_episode_config {
                                                  radians(eps_beta)                 (:249-256) */
   double radius_u_turn, turn_distance;                     /* :44; distance 2 (:565-567)   */
   double event_target_x, event_target_y;                   /* new_target(..., 2, 3) (:569) */
+  double incumbent0;       /* first optimal_criterion of an episode; 0 = control_criterion of
+                              the start pose with the episode's target.  The reference's is
+                              computed at import with config.py's target (:676):
+                              10000050990.195135                                          */
   int32_t p_turn_right, p_turn_left, p_new_target;         /* 60, 90, 110; <= 0 disables   */
   int32_t slow_new_target, slow_turn;                      /* slow_down(): 10, 20          */
-  int32_t max_steps;                                       /* restart after this many      */
+  int32_t max_steps;       /* > 0: restart after this many steps (a safeguard of long benches;
+                              the reference has none: 0 = run until on target or stuck)   */
+  int32_t enumerate;       /* sampled steps only: 1 = the reference's enumeration — candidate
+                              k < |V|*|B| is the constant sequence (V[k / |B|], B[k % |B|])
+                              (:311-317), candidates beyond the step's grid are padding with
+                              NaN controls (never chosen); 0 = constant prefix + hashed rest */
+  int32_t reserved_;
   uint64_t seed;                                           /* candidate sampler seed       */
 } mpc_episode_config_t;
+
+/* mpc_episode_log_t.status bits: what math_mpc's loop body (:542-574) did. */
+#define MPC_EP_STALE 1    /* no candidate beat the incumbent: the stale optimal_trajectory,
+                             result_v, result_beta were applied (:366-429)                 */
+#define MPC_EP_STUCK 2    /* the pose equals the previous one: recursive = True (:562-563)  */
+#define MPC_EP_BREAK 4    /* recursive was already set: "Recursive error", the episode ended
+                             before the events (:559-561); the next step restarts it        */
+#define MPC_EP_EVENT 8    /* an operator event fired at this p (:564-569)                   */
+#define MPC_EP_ARRIVED 16 /* on target after the step: the episode ended (:542)              */
+#define MPC_EP_LIMIT 32   /* max_steps reached: the episode restarts (not in the reference)  */
 
 typedef struct mpc_episode_log {
   int64_t step;          /* global MPC step counter                     */
   int64_t index;         /* chosen candidate (global), -1 if none       */
   int32_t p, episode;    /* iteration number within the episode         */
+  int32_t found;         /* a candidate beat the incumbent              */
+  int32_t status;        /* MPC_EP_* bits                               */
   double cost, x, y, phi, v, beta;   /* chosen cost and the state moved to */
 } mpc_episode_log_t;
 

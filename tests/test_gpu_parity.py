@@ -58,10 +58,12 @@ def _sampled(engine, n_cand, n_steps, seed=20261015, base=0):
 
 
 # --------------------------------------------------------------------------
-@pytest.mark.parametrize("integ", ["qk21", "rect"])
+@pytest.mark.parametrize("integ", ["qk21", "rect", "rect+rot", "rect+cum"])
 def test_scenario_replay_through_c_abi(engine, scenario, integ):
     """All 349 recorded predictive_control calls: identical (v, beta) and
-    index; states within 1e-9 of the reference's own."""
+    index; states within 1e-9 of the reference's own — for the reference's
+    arithmetic (qk21) and for the bench's (rect+cum, the chained step's
+    recurrence; rect+rot, the two-launch default of config E)."""
     worst = 0.0
     for rec in scenario["calls"]:
         v_sc, b_sc = call_controls(rec)
@@ -92,11 +94,14 @@ def test_coordinate_tree_states(engine, scenario, candidates):
             assert np.abs(got[layer] - ref).max() <= STATE_TOL
 
 
-def test_drop_in_scenario_end_to_end(engine, scenario):
+@pytest.mark.parametrize("integ", ["qk21", "rect+cum"])
+def test_drop_in_scenario_end_to_end(engine, scenario, integ, monkeypatch):
     """The whole reference scenario (math_model_tree.py:736-738) through the
     drop-in predictive_control/math_mpc: every call's chosen control and
-    returned state, the operator events and the episode trajectories."""
+    returned state, the operator events and the episode trajectories — with
+    the reference's arithmetic and with the bench's."""
     from diplomjourney_amd import math_model_tree as mmt
+    monkeypatch.setattr(mmt, "INTEGRATOR", integ)
     seen = []
     orig = mmt.predictive_control
 
@@ -155,6 +160,44 @@ def test_full_size_config_c(engine, oracle):
                                           incumbent=INC_MAX, integ="rect", want_costs=True)
     if _same_choice(got, ref, costs):
         _close_traj(got, ref, n_steps)
+
+
+def test_chained_config_c_steps_vs_oracle(engine, oracle):
+    """The bench's default step at config C's size: chained rect+cum launches
+    of the device episode (1e6 candidates, N = 10, distinct resident batches
+    drawn as bench.make_pool draws them).  Every logged step's winner is the
+    oracle's full scan (reference arithmetic, glibc trig) of the same batch on
+    the problem rebuilt on the host from the previous log record: chosen
+    index, (v, beta) identical, returned pose within 1e-9, cost within 1e-12."""
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.abi import make_problem
+    from diplomjourney_amd.episode import DeviceEpisode
+    n, ns, steps = 1_000_000, 10, 6
+    pool = _pool(engine, n, ns, steps, 0x5EED0000)
+    ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", chain=True, log_capacity=64)
+    for c in pool:
+        ep.step(controls=c)
+    ep.flush()
+    log = ep.read_log()
+    assert len(log) == steps and ep.chain_error() == 0
+    x = y = phi = 0.0
+    t = 0.0
+    for i, (rec, (v, b)) in enumerate(zip(log, pool)):
+        t = t + mmt.delta_t
+        prob = make_problem(x, y, phi, 2, 3, 0, 0, mmt.L, t, t + mmt.delta_t)
+        inc = 10000 * math.sqrt(13) + 10000 * 1000 ** 2 if i == 0 else INC_MAX
+        ref, costs, _ = oracle.rollout_argmin(prob, v.cpu().numpy(), b.cpu().numpy(),
+                                              incumbent=inc, integ="rect", want_costs=True)
+        assert (rec.p, rec.found, ref.found) == (i + 1, 1, 1)
+        if rec.index == ref.index:
+            assert (rec.v, rec.beta) == (ref.v, ref.beta)
+            assert math.isclose(rec.cost, ref.cost, rel_tol=COST_RTOL)
+            d = max(abs(a - c) for a, c in zip((rec.x, rec.y, rec.phi), ref.traj[0]))
+            assert d <= STATE_TOL, (i, d)
+        else:   # only a near-tie below the ulp noise of the two recurrences
+            gap = abs(costs[rec.index] - costs[ref.index]) / abs(costs[ref.index])
+            assert gap < 1e-13, (i, rec.index, ref.index, gap)
+        x, y, phi = rec.x, rec.y, rec.phi
 
 
 def test_sharded_exchange_equals_single_launch(engine):
@@ -344,29 +387,117 @@ def test_two_phase_api_matches(engine):
 @pytest.mark.parametrize("split", [False, True])
 def test_device_episode_matches_host_episode(engine, split):
     """The device-resident episode (mpc_episode_*: grid, sampler, problem,
-    finishing logic and operator events in HBM, no host sync) makes the same
-    choices as the host-driven episode over 200 MPC steps incl. the
-    p = 60 / 90 / 110 operator events — with the selection run by the last
+    finishing logic, stuck detector and operator events in HBM, no host sync)
+    makes the same choices as the host-driven episode over 200 MPC steps incl.
+    the p = 60 / 90 / 110 operator events — with the selection run by the last
     block of the rollout launch (fused) or by its own kernel (split)."""
     from diplomjourney_amd.episode import DeviceEpisode, Episode
     n, ns, steps = 20_000, 10, 200
     host = Episode(engine, n, ns)
     want = []
     for _ in range(steps):
-        p = host.p
-        r = host.step()
-        want.append((r.index if r.found else -1, r.cost, p, host.x, host.y, host.phi, host.v,
-                     host.beta))
+        host.step()
+        want.append(host.last_log)
     dev = DeviceEpisode(engine, n, ns, log_capacity=512, split=split)
     for _ in range(steps):
         dev.step()
     got = dev.read_log()
     assert len(got) == steps
     for g, w in zip(got, want):
-        assert (g.index, g.p) == (w[0], w[2])
+        assert (g.index, g.p, g.found, g.status) == (w[0], w[2], w[8], w[9])
         assert math.isclose(g.cost, w[1], rel_tol=COST_RTOL)
-        assert max(abs(a - b) for a, b in zip((g.x, g.y, g.phi, g.v, g.beta), w[3:])) <= STATE_TOL
+        assert max(abs(a - b) for a, b in zip((g.x, g.y, g.phi, g.v, g.beta), w[3:8])) <= STATE_TOL
     assert max(w[2] for w in want) > 110          # the operator events were exercised
+
+
+def _scenario_episode_log(engine, calls, integrator, n_cand=452):
+    """The device loop in the reference's configuration, one step per call."""
+    from diplomjourney_amd.episode import DeviceEpisode
+    ep = DeviceEpisode(engine, n_cand, 3, integrator=integrator, log_capacity=512,
+                       enumerate=True, incumbent0=10000050990.195135)
+    for _ in range(calls):
+        ep.step()
+    return ep.read_log()
+
+
+@pytest.mark.parametrize("integ", ["qk21", "rect+rot"])
+def test_device_episode_replays_reference_scenario(engine, scenario, integ):
+    """The device-resident math_mpc loop (mpc_episode_*: grids, slow-down,
+    enumeration, rollout, selection, finishing logic, stuck detector, operator
+    events, all in HBM, no host round trip) in the reference's configuration
+    — N = 3, the step's |V| x |B| constant sequences as the candidate set
+    (padding to 452 masked), the first incumbent of :676 — reproduces the
+    reference's model run (math_model_tree.py:736, calls 0-150): every
+    chosen (v, beta) identical, every returned pose within 1e-6, the events at
+    p = 60 / 90 / 110 and the arrival after call 150."""
+    from diplomjourney_amd.abi import MPC_EP_ARRIVED, MPC_EP_EVENT
+    calls = [c for c in scenario["calls"] if not c["isActual"]]
+    assert len(calls) == 151
+    log = _scenario_episode_log(engine, len(calls), integ)
+    assert len(log) == len(calls)
+    worst = 0.0
+    for i, (rec, g) in enumerate(zip(calls, log)):
+        assert (g.p, g.episode, g.found) == (i + 1, 1, int(rec["found"]))
+        assert (g.v, g.beta) == tuple(rec["ret"][3:5]), i
+        worst = max(worst, max(abs(a - b) for a, b in zip((g.x, g.y, g.phi), rec["ret"][:3])))
+        V, B = rec["V"], rec["B"]
+        if rec["pre"]["steps_for_slowing"] > 0:                 # :312-316
+            V = [min(V) if min(V) > 0.4 else 0.4] * len(V)
+        first = next(k for k in range(len(V) * len(B))          # lowest index of the control
+                     if (V[k // len(B)], B[k % len(B)]) == (g.v, g.beta))
+        assert g.index == first, i
+        want = MPC_EP_EVENT if g.p in (60, 90, 110) else 0
+        want |= MPC_EP_ARRIVED if i == len(calls) - 1 else 0
+        assert g.status == want, (i, g.status)
+    assert worst <= 1e-6, worst
+def test_device_episode_stuck_detector_vs_drop_in(engine):
+    """A target behind the robot: after one forced move (the line-origin
+    sentinel makes staying at the start cost 1e10) staying still is optimal,
+    the pose repeats (recursive = True, :562-563) and the next step ends the
+    episode with "Recursive error" (:559-561).  The device loop logs the same
+    three steps as the drop-in math_mpc (chosen control, pose, p), marks them
+    stuck / break, and restarts the episode after the break."""
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.abi import MPC_EP_BREAK, MPC_EP_STUCK
+    from diplomjourney_amd.episode import DeviceEpisode
+    mmt.reset_state()
+    inc0 = mmt.optimal_criterion
+    seen = []
+    try:
+        mmt.math_mpc([0, 0, 0, 0, 0], [-2, 0], False, on_step=lambda p, c: seen.append((p, c)))
+        assert mmt.recursive
+    finally:
+        mmt.reset_state()
+    assert [p for p, _ in seen] == [1, 2, 3]
+    ep = DeviceEpisode(engine, 452, 3, integrator="qk21", log_capacity=16, target=(-2, 0),
+                       enumerate=True, incumbent0=inc0)
+    for _ in range(4):
+        ep.step()
+    log = ep.read_log()
+    for (p, c), g, st in zip(seen, log, (0, MPC_EP_STUCK, MPC_EP_BREAK)):
+        assert (g.p, g.episode, g.status, g.found) == (p, 1, st, 1)
+        assert (g.v, g.beta) == (c[3], c[4])
+        assert max(abs(a - b) for a, b in zip((g.x, g.y, g.phi), c[:3])) <= 1e-6
+    assert (log[3].p, log[3].episode) == (1, 2)        # the ended episode restarted
+
+
+def test_device_episode_stale_without_winner(engine):
+    """No candidate beats the incumbent (incumbent0 below every cost): the
+    step keeps the stale optimal_trajectory — before any winner, the pose
+    itself (the reference's [[[0]]] has no layers to return) — so the pose
+    repeats (stuck); the next step finds a winner but ends the episode
+    (recursive was set).  The host-driven Episode applies the same update."""
+    from diplomjourney_amd.abi import MPC_EP_BREAK, MPC_EP_STALE, MPC_EP_STUCK
+    from diplomjourney_amd.episode import DeviceEpisode
+    ep = DeviceEpisode(engine, 452, 3, integrator="qk21", log_capacity=16, enumerate=True,
+                       incumbent0=1.0)
+    for _ in range(3):
+        ep.step()
+    a, b, c = ep.read_log()
+    assert (a.found, a.index, a.status, a.p) == (0, -1, MPC_EP_STALE | MPC_EP_STUCK, 1)
+    assert (a.x, a.y, a.phi, a.v, a.beta) == (0.0, 0.0, 0.0, 0.0, 0.0)
+    assert (b.found, b.status, b.p, b.episode) == (1, MPC_EP_BREAK, 2, 1)
+    assert (c.p, c.episode) == (1, 2)
 
 
 @pytest.mark.parametrize("integ", ["rect+rot", "qk21", "rect", "qk21+rot"])
