@@ -56,6 +56,10 @@ METRIC = "candidate N-step rollouts/sec + MPC-step p50 latency, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 WORKLOADS = {
+    "A": dict(n_steps=3, per_gpu=None,
+              desc="config A: the reference scenario (math_model_tree.py:736-738, 349 "
+                   "predictive_control calls, N=3, the acceleration-limited grid <= 451 "
+                   "candidates) through the drop-in predictive_control"),
     "B": dict(n_steps=3, per_gpu=100_000, desc="config B: N=3, 1e5 candidates/GPU, episode"),
     "C": dict(n_steps=10, per_gpu=1_000_000,
               desc="config C: N=10, 1e6 candidates/GPU, moving-target episode"),
@@ -85,7 +89,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=None,
                     help="timed steps (default 500 for the ~40 us expansion workloads, so the "
                          "fixed graph-launch + sync cost (~0.2 ms) is amortised; 50 for F/G)")
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps first (default 20; 1 scenario run for workload A)")
     ap.add_argument("--workload", default="C", choices=sorted(WORKLOADS))
     ap.add_argument("--integrator", default=None,
                     choices=["rect+cum", "rect+rot", "rect", "qk21+rot", "qk21"],
@@ -128,10 +133,12 @@ def parse():
                          "(tools/pmc.sh + tools/pmc_summary.py on the same kernel and config; "
                          "default: the committed round-2 summary of the roofline's kernel)")
     args = ap.parse_args()
-    if args.integrator is None:
+    if args.integrator is None and args.workload != "A":   # A: the drop-in's default (qk21)
         args.integrator = "rect+cum" if args.workload in ("B", "C", "D") else "rect+rot"
+    if args.warmup is None:
+        args.warmup = 1 if args.workload == "A" else 20
     if args.steps is None:
-        args.steps = 50 if args.workload in ("F", "G") else 500
+        args.steps = 50 if args.workload in ("F", "G") else 3 if args.workload == "A" else 500
     return args
 
 
@@ -169,10 +176,132 @@ def cpu_baseline(wl, seconds):
     prob = (0.0, 0.0, 0.0, 2, 3, 0, 0, 0.5, 0.05, 0.1)
     r = cpu_ref.timed_rate(prob, v, b, budget_s=seconds)
     return {"value": r["rate"], "unit": "rollouts/s", "cores": r["cores"], "kind": "port",
+            "affinity_cpus": r.get("affinity_cpus"), "cgroup_cpu_quota": r.get("cgroup_cpu_quota"),
             "sample": (f"{r['candidates']} sampled N={n_steps} candidates of the first MPC step "
                        f"(reference grid around v=0, beta=0), scipy.integrate.quad per "
-                       f"integral as math_model_tree.py:91-115, {r['cores']} processes x "
-                       f"{seconds:.0f} s budget, busy {r['busy_s']:.1f} s")}
+                       f"integral as math_model_tree.py:91-115, {r['cores']} processes (every "
+                       f"granted core: affinity {r.get('affinity_cpus')}, cgroup quota "
+                       f"{r.get('cgroup_cpu_quota')}) x {seconds:.0f} s budget, busy "
+                       f"{r['busy_s']:.1f} s")}
+
+
+def _scenario_calls():
+    """The reference's 349 recorded predictive_control calls (tests/golden,
+    generated by running the reference; data only)."""
+    with open(os.path.join(REPO, "tests", "golden", "reference_scenario.json")) as fh:
+        return json.load(fh)["calls"]
+
+
+def _call_controls(rec):
+    """Candidate SoA [3, |V||B|] of one recorded call (slow-down :312-316)."""
+    import numpy as np
+    V, B = list(rec["V"]), list(rec["B"])
+    if rec["pre"]["steps_for_slowing"] > 0:
+        V = [min(V) if min(V) > 0.4 else 0.4] * len(V)
+    vv = np.repeat(np.array(V, dtype=np.float64), len(B))
+    bb = np.tile(np.array(B, dtype=np.float64), len(V))
+    return np.tile(vv, (3, 1)), np.tile(bb, (3, 1))
+
+
+def cpu_baseline_dropin(seconds):
+    """Config A on one host core (the reference is single-threaded): the
+    reference-structured port of predictive_control (oracle/cpu_ref.py,
+    scipy.integrate.quad per integral, strict-< scan) on the recorded calls
+    in order until the budget is spent — p50 of the expansion alone (the
+    reference's own timer, :307 -> :362) and with the reference's
+    CoordinateTree allocation of S1 + S1^2 + S1^3 object slots
+    (CoordinateTree.py:5-9, freed after the call)."""
+    import numpy as np
+    from oracle import cpu_ref
+    calls = _scenario_calls()
+    exp_ms, e2e_ms, cands = [], [], 0
+    t_start = time.perf_counter()
+    for rec in calls:
+        if time.perf_counter() - t_start > seconds:
+            break
+        v, b = _call_controls(rec)
+        s1 = v.shape[1]
+        pre, t = rec["pre"], rec["post"]["t"]
+        prob = (rec["x"], rec["y"], rec["phi"], pre["x_t"], pre["y_t"], pre["x_0"], pre["y_0"],
+                0.5, t, t + 0.05)
+        t0 = time.perf_counter()
+        tree = np.empty(s1 + s1 * s1 + s1 * s1 * s1, dtype=object)
+        t1 = time.perf_counter()
+        cpu_ref.expand(prob, v, b, 0, s1, incumbent=pre["optimal_criterion"])
+        t2 = time.perf_counter()
+        del tree
+        t3 = time.perf_counter()
+        exp_ms.append((t2 - t1) * 1e3)
+        e2e_ms.append((t3 - t0) * 1e3)
+        cands += s1
+    from diplomjourney_amd.episode import percentile
+    return {"value": percentile(e2e_ms, 50), "unit": "ms per MPC step (p50)", "cores": 1,
+            "kind": "port", "p50_expansion_ms": percentile(exp_ms, 50),
+            "rollouts_per_s_expansion": cands / (sum(exp_ms) * 1e-3),
+            "sample": (f"the first {len(e2e_ms)} recorded reference calls ({cands} N=3 "
+                       f"candidates), predictive_control's expansion as the reference runs it "
+                       f"(scipy quad per integral) + its CoordinateTree allocation, one core")}
+
+
+def bench_dropin(args, wl, eng, rank, world, cpu):
+    """Config A: the reference scenario through the drop-in math_mpc /
+    predictive_control (host episode loop, one C-ABI expansion + one 808-B
+    read per call, as the reference calls it).  Parity against the recorded
+    calls; p50 of predictive_control (host time, end to end) over --steps
+    scenario runs after --warmup ones."""
+    import torch
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.episode import percentile
+    mmt.INTEGRATOR = "qk21" if args.integrator is None else args.integrator
+    calls = _scenario_calls()
+    ms, rets = [], []
+    orig = mmt.predictive_control
+
+    def timed(*a):
+        t0 = time.perf_counter()
+        r = orig(*a)
+        ms.append((time.perf_counter() - t0) * 1e3)
+        rets.append(r)
+        return r
+    mmt.predictive_control = timed
+    try:
+        for _ in range(args.warmup):
+            mmt.run_reference_scenario(seed=0)
+        ms.clear()
+        rets.clear()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            mmt.run_reference_scenario(seed=0)
+        elapsed = time.perf_counter() - t0
+    finally:
+        mmt.predictive_control = orig
+        mmt.reset_state()
+    n_calls = len(rets)
+    same = worst = 0
+    for i, r in enumerate(rets):
+        want = calls[i % len(calls)]["ret"]
+        same += r[3:] == want[3:]
+        worst = max(worst, max(abs(a - b) for a, b in zip(r[:3], want[:3])))
+    cands = sum(len(c["V"]) * len(c["B"]) for c in calls) * args.steps
+    out = {
+        "metric": METRIC, "value": cands / elapsed, "unit": "rollouts/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / n_calls * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "the reference's own scenario (recorded inputs, tests/golden)",
+        "config": {"workload": wl["desc"], "n_steps": 3, "calls_per_run": len(calls),
+                   "integrator": mmt.INTEGRATOR if args.integrator is None else args.integrator,
+                   "step": "drop-in predictive_control: host grid + candidate SoA upload, one "
+                           "expansion launch pair (CoordinateTree states out), one 808-B read"},
+        "p50_ms": percentile(ms, 50), "p90_ms": percentile(ms, 90),
+        "p50_note": "host time per predictive_control call, end to end (the reference's "
+                    "0.361 s p50 is the same call on one CPU core, SURVEY §6)",
+        "parity": {"calls": n_calls, "chosen_control_identical": same,
+                   "max_abs_pose_diff": worst},
+        "roofline": None, "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 def main():
@@ -184,6 +313,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = (cpu_baseline_fulltree(args.cpu_seconds) if args.workload in ("F", "G")
+               else cpu_baseline_dropin(args.cpu_seconds) if args.workload == "A"
                else cpu_baseline(wl, args.cpu_seconds))
 
     import torch
@@ -202,6 +332,8 @@ def main():
     from diplomjourney_amd.expansion import Expansion
     eng = Expansion(device)
 
+    if args.workload == "A":
+        return bench_dropin(args, wl, eng, rank, world, cpu)
     if args.workload == "E":
         return bench_robots(args, wl, eng, rank, world, cpu)
     if args.workload == "F":
@@ -263,7 +395,15 @@ def main():
             ep.generate = False
             generated = {"inputs": "generated", "value": n_total * args.steps / r["elapsed"],
                          "ms_per_step": r["elapsed"] / args.steps * 1e3,
-                         "p50_ms": r["p50_ms"]}
+                         "p50_ms": r["p50_ms"],
+                         "roofline_valu": valu_roofline(
+                             "k_rollout_generated", args.integrator,
+                             r["elapsed"] / args.steps * 1e3, n_total // world, n_steps,
+                             note="over the whole step (generated rollout + selection): a "
+                                  "lower bound of the rollout kernel's rate")}
+    host_ms = None
+    if not args.host_loop and not exchange:
+        host_ms = host_latency_pass(ep, pool)
     elapsed = main_run["elapsed"]
     bytes_launch = 16.0 * n_steps * ep.n_local
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
@@ -302,22 +442,33 @@ def main():
                                                                    if exchange else "")},
         "p50_ms": main_run["p50_ms"], "p90_ms": main_run["p90_ms"],
         "p50_note": "GPU time per MPC step (HIP events between step starts, eager launches)",
+        "p50_host_ms": percentile(host_ms, 50) if host_ms else None,
+        "p90_host_ms": percentile(host_ms, 90) if host_ms else None,
+        "p50_host_note": ("host time per eager MPC step until its 808-B result record is in "
+                          "pinned host memory (step launches + completion + D2H + sync), as a "
+                          "controller receives the chosen control (math_model_tree.py:429); "
+                          "reference: 0.361 s p50 per predictive_control at N=3, 451 "
+                          "candidates (SURVEY §6)"),
         "kernel_ms": kern_ms, "kernel_in_step_ms": main_run["kernel_in_step_ms"],
         "roofline": (None if inputs == "generated" else
                      roofline(achieved, bytes_launch, args.traffic_json, kernel=kernel)),
         "roofline_rollout_only": (None if rollout_ms is None else
                                   roofline(bytes_launch / (rollout_ms * 1e-3) / 1e9, bytes_launch,
                                            None, kernel="k_rollout_argmin_stream")),
+        "roofline_valu": valu_roofline(kernel, args.integrator, kern_ms, n_total // world,
+                                       n_steps),
         "other_inputs": other,
         "generated_inputs": generated,
         "cpu_baseline": cpu,
     }
     if out["roofline"] is not None and pool is not None:
-        # the same kernel against a measured copy ceiling and
-        # its VALU issue share (PMC counters of the committed traffic summary)
-        ceil = copy_ceiling(pool)
-        out["roofline"]["copy_ceiling_GBs"] = ceil
-        out["roofline"]["frac_of_copy_ceiling"] = achieved / ceil
+        # the same kernel against the measured read ceiling of
+        # its own access pattern and its VALU issue share (PMC counters of the
+        # committed traffic summary)
+        ceil, ceil_ms = stream_ceiling(ep, pool)
+        out["roofline"]["stream_ceiling_GBs"] = ceil
+        out["roofline"]["stream_ceiling_ms"] = ceil_ms
+        out["roofline"]["frac_of_stream_ceiling"] = achieved / ceil
         out["roofline"]["valu"] = valu_share(args.traffic_json, kernel, bytes_launch, kern_ms)
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -325,24 +476,62 @@ def main():
         dist.destroy_process_group()
 
 
-def copy_ceiling(pool, reps=20):
-    """Measured HBM ceiling on this GPU: device-to-device copies of the
-    resident batches' v rows into a scratch buffer (rotating over the pool, so
-    no source is cache-resident), HIP events; GB/s of bytes read + written."""
+def stream_ceiling(ep, pool, reps=100, warm=100):
+    """Measured read ceiling of the rollout's own access pattern on this GPU:
+    mpc_stream_probe (the streaming kernel's grid, tiles and LDS-DMA control
+    ring, no arithmetic) over the same resident batches, REPS back-to-back
+    launches between HIP events on the episode's stream, rotating over the
+    pool as kernel_pass does.  Returns (GB/s of the 16 B per candidate-step
+    read, ms per launch)."""
+    import ctypes
     import torch
-    src = [v for v, _ in pool]
-    dst = torch.empty_like(src[0])
-    for i in range(4):
-        dst.copy_(src[i % len(src)])
+    lib = ep.lib
+    n, ns = ep.n_local, ep.n_steps
+    grid = min(-(-n // 512), 2048)
+    sink = torch.empty(grid * 256, dtype=torch.int64, device=pool[0][0].device)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def one(i):
+        v, b = pool[i % len(pool)]
+        rc = lib.mpc_stream_probe(v.data_ptr(), b.data_ptr(), n, ns, sink.data_ptr(),
+                                  sink.numel() * 8, st)
+        if rc != 0:
+            raise RuntimeError(f"mpc_stream_probe: status {rc}")
+    for i in range(warm):
+        one(i)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for i in range(reps):
-        dst.copy_(src[(i + 1) % len(src)])
+        one(i + 1)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    del dst
-    return 2.0 * src[0].numel() * 8 / (ms * 1e-3) / 1e9
+    return 16.0 * ns * n / (ms * 1e-3) / 1e9, ms
+
+
+def host_latency_pass(ep, pool, n=200):
+    """The latency a controller sees (the reference returns the chosen
+    control to its caller every step, math_model_tree.py:429): per eager MPC
+    step, host time from enqueueing the step until its 808-B result record is
+    in pinned host memory — the step's launches (a chained step is completed
+    by its flush launch), the D2H copy and the stream sync.  Episode state
+    stays on the device; returns the per-step host times in ms."""
+    import torch
+    host = torch.empty(ep.local.numel(), dtype=torch.uint8).pin_memory()
+    stream = torch.cuda.current_stream()
+    out = []
+    for i in range(n + 20):
+        t0 = time.perf_counter()
+        if pool is None:
+            ep.step()
+        else:
+            ep.step(controls=pool[i % len(pool)])
+        ep.flush()
+        host.copy_(ep.local, non_blocking=True)
+        stream.synchronize()
+        if i >= 20:
+            out.append((time.perf_counter() - t0) * 1e3)
+    return out
 
 
 def valu_share(traffic_json, kernel, bytes_launch, kern_ms):
@@ -510,6 +699,45 @@ def kernel_pass(ep, pool, reps=100, warm=200):
 
 TRAFFIC_JSON = {"k_rollout_argmin_stream": "r02_traffic.json",
                 "k_episode_chain": "r02_traffic_chain.json"}
+
+# fp64 VALU counters (tools/pmc_valu.sh: SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F64,
+# SQ_INSTS_VALU) of each kernel at the size it was measured on:
+# (kernel, integrator) -> (summary, candidates, horizon) — config C, or the
+# S1 = 451 full tree of config F (candidates = leaves)
+VALU_JSON = {("k_episode_chain", "rect+cum"): ("r03_valu_chain.json", 1_000_000, 10),
+             ("k_rollout_argmin_stream", "qk21"): ("r03_valu_qk21.json", 1_000_000, 10),
+             ("k_rollout_generated", "rect+cum"): ("r03_valu_gen.json", 1_000_000, 10),
+             ("k_ft_leaves", "rect+rot"): ("r03_valu_ft.json", 451 ** 3, 3)}
+
+
+def valu_roofline(kernel, integrator, ms, n_cand, n_steps, note=None):
+    """SURVEY §8(d)'s second roofline: fp64 operations per launch from the
+    committed PMC counters (64 lanes x (2 FMA + ADD + MUL + TRANS) per
+    wave-instruction; inactive lanes counted, so an upper bound) over the
+    measured duration, against the 78.6 TFLOP/s fp64 vector peak; and the
+    VALU issue share (all VALU wave-instructions at 4 cycles on 1024 SIMDs at
+    2.4 GHz).  None when no summary was measured for this kernel and size."""
+    spec = VALU_JSON.get((kernel, integrator))
+    if spec is None or spec[1] != n_cand or spec[2] != n_steps or not ms:
+        return None
+    path = os.path.join(REPO, "profiles", spec[0])
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        t = json.load(fh)
+    ops = t.get("fp64_ops_per_launch")
+    insts = t.get("counters_median_per_launch", {}).get("SQ_INSTS_VALU")
+    if not ops or t.get("kernel") != kernel:
+        return None
+    tf = ops / (ms * 1e-3) / 1e12
+    out = {"bound": "valu-fp64", "achieved": tf, "peak": FP64_VECTOR_PEAK_TFLOPS,
+           "unit": "TFLOP/s", "frac": tf / FP64_VECTOR_PEAK_TFLOPS, "kernel": kernel,
+           "fp64_ops_per_launch": ops,
+           "valu_issue_share": (insts * 4.0 / (1024 * 2.4e9 * ms * 1e-3)) if insts else None,
+           "source": os.path.relpath(path, REPO)}
+    if note:
+        out["note"] = note
+    return out
 
 
 def chain_pass(ep, pool, reps=100, warm=200):
@@ -706,6 +934,10 @@ def bench_fulltree(args, wl, eng, rank, world, cpu):
                      "kernel": "k_ft_leaves",
                      "note": "algorithmic fp64 ops per leaf as written (FT_FLOPS_PER_LEAF); "
                              "leaves are generated from the index, no HBM stream"},
+        "roofline_valu": valu_roofline("k_ft_leaves", args.integrator, per_step * 1e3 * world,
+                                       leaves, 3,
+                                       note="counted fp64 ops of one MPC step (all leaves) over "
+                                            "the step's host time x ranks: a lower bound"),
         "cpu_baseline": cpu,
     }
     if rank == 0:

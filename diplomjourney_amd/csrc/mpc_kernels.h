@@ -444,6 +444,57 @@ __global__ __launch_bounds__(kBlock, kStreamWaves) void k_rollout_argmin_stream(
                                                           part, nullptr);
 }
 
+// Measurement probe (mpc_stream_probe): the streaming kernel's memory side
+// alone — the same grid, tiles, lanes and LDS-DMA control ring (kRing slots,
+// kRing-1 steps in flight, `nt`), each landed slot read back from LDS and
+// folded into one word per lane, no rollout arithmetic.  Its duration is the
+// read-only stream ceiling of the rollout's own access pattern at the
+// launch's size (launch ramp and tail included), the denominator the
+// streaming kernels' time is compared with.
+__global__ __launch_bounds__(kBlock, kStreamWaves) void k_stream_probe(
+    const double* __restrict__ v, const double* __restrict__ b, int64_t n_cand, int n_steps,
+    uint64_t* __restrict__ sink) {
+  constexpr int R = kRing;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t ring0 = __builtin_amdgcn_readfirstlane(lds_addr(&g_ring[wv][0][0][0]));
+  constexpr uint32_t kSlot = 2 * 64 * sizeof(double2);
+  auto dst = [&](int slot) { return ring0 + slot * kSlot; };
+  const int64_t n_tiles = (n_cand + kBlock * 2 - 1) / (kBlock * 2);
+  uint64_t acc = 0;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int64_t c0 = tile * (kBlock * 2) + threadIdx.x * 2;
+    if (c0 >= n_cand) continue;   // n_cand even (host check): the pair is valid
+#pragma unroll
+    for (int u = 0; u < R - 1; ++u)
+      if (u < n_steps) glds_pair(v + u * n_cand + c0, b + u * n_cand + c0, dst(u),
+                                 dst(u) + kSlot / 2);
+    double2 v2 = make_double2(0.0, 0.0), b2 = v2;
+#pragma unroll 1
+    for (int s = 0; s < n_steps; s += R) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const int st = s + u;
+        if (st < n_steps) {
+          if (st + R - 1 < n_steps) {
+            const int sr = st + R - 1, slot = (u + R - 1) % R;
+            glds_refill(v + sr * n_cand + c0, b + sr * n_cand + c0, dst(slot),
+                        dst(slot) + kSlot / 2, v2, b2);
+            wait_vm<2 * (R - 1)>();
+          } else {
+            wait_vm<0>();
+          }
+          v2 = g_ring[wv][u][0][lane];
+          b2 = g_ring[wv][u][1][lane];
+          acc ^= static_cast<uint64_t>(__double_as_longlong(v2.x)) ^
+                 static_cast<uint64_t>(__double_as_longlong(b2.y));
+        }
+      }
+    }
+  }
+  if (acc == 0x5eedull) sink[blockIdx.x * kBlock + threadIdx.x] = acc;   // keeps the reads live
+}
+
 // What the episode update needs of a winner (kept in registers by the
 // finalize kernel instead of being re-read from the result record).
 struct Winner {

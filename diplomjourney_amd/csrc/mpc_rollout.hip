@@ -329,6 +329,18 @@ int mpc_rollout_argmin_batched(const mpc_problem_t* problems, const double* incu
   return last_hip_status();
 }
 
+int mpc_stream_probe(const double* v_sc, const double* beta_sc, int64_t n_cand,
+                     int32_t n_steps, void* sink, size_t sink_bytes, mpc_stream_t stream) {
+  if (!v_sc || !beta_sc || n_cand < 2 || n_steps < 1 || n_steps > MPC_MAX_STEPS || !sink)
+    return MPC_ERR_ARG;
+  if (!wide_ok(v_sc, beta_sc, n_cand)) return MPC_ERR_UNSUPPORTED;
+  const int64_t grid = rollout_grid<kCplWide>(n_cand);
+  if (sink_bytes < static_cast<size_t>(grid) * kBlock * sizeof(uint64_t)) return MPC_ERR_WORKSPACE;
+  k_stream_probe<<<grid, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+      v_sc, beta_sc, n_cand, n_steps, static_cast<uint64_t*>(sink));
+  return last_hip_status();
+}
+
 int mpc_select_winner(const mpc_result_t* results, int32_t n, double incumbent,
                       mpc_result_t* out, mpc_stream_t stream) {
   if (!results || !out || n < 1) return MPC_ERR_ARG;

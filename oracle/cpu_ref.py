@@ -82,12 +82,40 @@ def _timed_worker(args):
     return done - lo, time.perf_counter() - t0, best
 
 
+def granted_cores():
+    """The host cores this process may use: its CPU affinity, bounded by the
+    cgroup's CPU quota when one is set (a GPU box's share of a large host
+    shows the whole machine in its affinity mask; the quota is the grant).
+    Returns (cores, evidence dict)."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):                       # cgroup v2
+        try:
+            q, period = open(path).read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(period)
+        except (OSError, ValueError):
+            pass
+    if quota is None:                                              # cgroup v1
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / period
+        except (OSError, ValueError):
+            pass
+    cores = affinity if quota is None else max(1, min(affinity, int(quota + 0.5)))
+    return cores, {"affinity_cpus": affinity, "cgroup_cpu_quota": quota}
+
+
 def timed_rate(problem, v_sc, b_sc, budget_s=10.0, cores=None, max_per_core=40_000):
-    """Candidates/s of the port on `cores` processes, each scanning its own
-    contiguous slice of the candidate set for ~budget_s seconds."""
+    """Candidates/s of the port on `cores` processes (default: every core the
+    host grants, granted_cores()), each scanning its own contiguous slice of
+    the candidate set for ~budget_s seconds."""
     import multiprocessing as mp
+    evidence = {}
     if cores is None:
-        cores = max(1, min(16, len(os.sched_getaffinity(0))))
+        cores, evidence = granted_cores()
     v_sc, b_sc = np.asarray(v_sc), np.asarray(b_sc)
     n = v_sc.shape[1]
     per = max(1, n // cores)
@@ -104,4 +132,4 @@ def timed_rate(problem, v_sc, b_sc, budget_s=10.0, cores=None, max_per_core=40_0
     done = sum(o[0] for o in outs)
     busy = max(o[1] for o in outs)
     return {"candidates": done, "wall_s": wall, "busy_s": busy, "cores": cores,
-            "rate": done / busy}
+            "rate": done / busy, **evidence}

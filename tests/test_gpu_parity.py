@@ -742,9 +742,11 @@ def test_bench_contract(extra):
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] < 1
     assert rf["algorithmic_bytes_per_launch"] == 16.0 * 10 * 1_000_000
-    # a measured copy ceiling beside the spec peak, and the
+    # the measured read ceiling of the kernel's own access
+    # pattern beside the spec peak, the host-visible step latency, and the
     # kernel's VALU issue share from the committed PMC counters
-    assert 2000 < rf["copy_ceiling_GBs"] < 9000 and 0 < rf["frac_of_copy_ceiling"] < 1.5
+    assert 2000 < rf["stream_ceiling_GBs"] < 9000 and 0 < rf["frac_of_stream_ceiling"] < 1.5
+    assert 0 < d["p50_host_ms"] < 5
     assert 0 < rf["valu"]["fp64_issue_share"] < 1.5
     if extra:
         assert d["config"]["integrator"] == "rect+rot"
@@ -756,6 +758,22 @@ def test_bench_contract(extra):
         ro = d["roofline_rollout_only"]
         assert ro["kernel"] == "k_rollout_argmin_stream" and 0 < ro["frac"] < 1
     assert rf["traffic"] is not None and abs(rf["traffic"] / 160e6 - 1) < 0.01
+
+
+def test_bench_workload_a_parity():
+    """bench.py --workload A: the reference scenario through the drop-in,
+    one JSON line with every recorded call's chosen control identical."""
+    import json
+    import os
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--workload", "A",
+                        "--steps", "1", "--warmup", "0", "--cpu-seconds", "0"],
+                       capture_output=True, text=True, timeout=200, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["parity"]["calls"] == 349 == d["parity"]["chosen_control_identical"]
+    assert d["parity"]["max_abs_pose_diff"] <= 1e-6 and d["p50_ms"] > 0
 
 
 @pytest.mark.parametrize("integ,n,L", [("rect+cum", 100_000, None), ("rect+rot", 100_000, None),

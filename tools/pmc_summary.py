@@ -30,8 +30,15 @@ def main():
         med[name] = xs[len(xs) // 2]
     fetch_b = med.get("FETCH_SIZE", 0.0) * 1024.0
     write_b = med.get("WRITE_SIZE", 0.0) * 1024.0
+    f64 = None
+    if "SQ_INSTS_VALU_FMA_F64" in med:
+        # fp64 operations per launch, 64 lanes per wave-instruction (an upper
+        # bound: inactive lanes count); FMA = 2
+        f64 = 64.0 * (2 * med["SQ_INSTS_VALU_FMA_F64"] + med.get("SQ_INSTS_VALU_ADD_F64", 0)
+                      + med.get("SQ_INSTS_VALU_MUL_F64", 0) + med.get("SQ_INSTS_VALU_TRANS_F64", 0))
     res = {
         "kernel": kernel,
+        "fp64_ops_per_launch": f64,
         "hbm_bytes_per_launch": 2.0 * fetch_b + write_b,
         "algorithmic_bytes_per_launch": algo,
         "fetch_size_bytes_raw": fetch_b, "write_size_bytes": write_b,

@@ -4,7 +4,10 @@ batches, then launch only the rollout kernel `reps` times rotating over them
 launches stream from HBM as in the bench).
     python tools/prof_kernel.py [n_cand] [n_steps] [integ] [reps] [batches]
 integ "chain": chained rect+cum episode steps instead (mpc_episode_chain_step,
-the bench default's launch: rollout of step k + completion of step k-1)."""
+the bench default's launch: rollout of step k + completion of step k-1);
+"generated": generated-controls episode steps (k_rollout_generated, rect+cum);
+"fulltree": config F's full-tree MPC steps (k_ft_leaves, S1 = 451, n_cand and
+n_steps ignored)."""
 import os
 import sys
 
@@ -25,6 +28,26 @@ def main():
     reps = int(sys.argv[4]) if len(sys.argv) > 4 else 20
     nb = int(sys.argv[5]) if len(sys.argv) > 5 else 4
     eng = Expansion("cuda:0")
+    if integ == "fulltree":
+        import math
+        from diplomjourney_amd import run_math_model as rmm
+        rmm.INTEGRATOR = "rect+rot"
+        rmm.configure(0.1, math.radians(3))
+        rmm.start_episode(-3.0, -2.0, 0.3, 4.0, 5.0)
+        for _ in range(reps):
+            c = rmm.predictive_control(rmm.x, rmm.y, rmm.phi, rmm.v, rmm.x_t, rmm.y_t)
+            rmm.x, rmm.y, rmm.phi, rmm.v, rmm.beta = c
+        torch.cuda.synchronize()
+        print("done fulltree", reps)
+        return
+    if integ == "generated":
+        from diplomjourney_amd.episode import DeviceEpisode
+        ep = DeviceEpisode(eng, n, ns, integrator="rect+cum", generate=True, log_capacity=8192)
+        for i in range(reps):
+            ep.step()
+        torch.cuda.synchronize()
+        print("done generated", n, ns, reps)
+        return
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
     pool = [eng.sample_controls(V, B, n, ns, 7 + i) for i in range(nb)]
