@@ -72,6 +72,11 @@ WORKLOADS = {
                    "S1^3 = 9.17e7 leaves per MPC step, heading-term criterion, never-reset "
                    "incumbent; episode of the run_math_model drop-in"),
 }
+WORKLOADS["R"] = dict(n_steps=3, per_gpu=None, robots=1000,
+                      desc="run_math_model.py's 1000-episode loop (:231-280) over the tree "
+                           "expansion of math_model_tree.py (acceleration-limited grid <= 451 "
+                           "candidates, N=3): one robot per episode, lockstep, one batched "
+                           "launch pair per MPC step (mpc_rollout_argmin_batched)")
 WORKLOADS["G"] = dict(n_steps=3, per_gpu=None, robots=1000,
                       desc="run_math_model.py's 1000 episodes (SURVEY 8f 4): one robot per "
                            "episode, lockstep, one batched full-tree launch per MPC step, "
@@ -133,12 +138,15 @@ def parse():
                          "(tools/pmc.sh + tools/pmc_summary.py on the same kernel and config; "
                          "default: the committed round-2 summary of the roofline's kernel)")
     args = ap.parse_args()
-    if args.integrator is None and args.workload != "A":   # A: the drop-in's default (qk21)
+    if args.integrator is None and args.workload in ("A", "R"):
+        args.integrator = "qk21"          # the drop-in's default: the reference's arithmetic
+    if args.integrator is None:
         args.integrator = "rect+cum" if args.workload in ("B", "C", "D") else "rect+rot"
     if args.warmup is None:
-        args.warmup = 1 if args.workload == "A" else 20
+        args.warmup = 1 if args.workload == "A" else 5 if args.workload == "R" else 20
     if args.steps is None:
-        args.steps = 50 if args.workload in ("F", "G") else 3 if args.workload == "A" else 500
+        args.steps = (50 if args.workload in ("F", "G") else 3 if args.workload == "A"
+                      else 1000 if args.workload == "R" else 500)
     return args
 
 
@@ -313,7 +321,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = (cpu_baseline_fulltree(args.cpu_seconds) if args.workload in ("F", "G")
-               else cpu_baseline_dropin(args.cpu_seconds) if args.workload == "A"
+               else cpu_baseline_dropin(args.cpu_seconds) if args.workload in ("A", "R")
                else cpu_baseline(wl, args.cpu_seconds))
 
     import torch
@@ -336,6 +344,8 @@ def main():
         return bench_dropin(args, wl, eng, rank, world, cpu)
     if args.workload == "E":
         return bench_robots(args, wl, eng, rank, world, cpu)
+    if args.workload == "R":
+        return bench_tree_episodes(args, wl, eng, rank, world, cpu)
     if args.workload == "F":
         return bench_fulltree(args, wl, eng, rank, world, cpu)
     if args.workload == "G":
@@ -939,6 +949,67 @@ def bench_fulltree(args, wl, eng, rank, world, cpu):
                                        note="counted fp64 ops of one MPC step (all leaves) over "
                                             "the step's host time x ranks: a lower bound"),
         "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_tree_episodes(args, wl, eng, rank, world, cpu):
+    """The named entry: run_math_model.py's seeded episode loop
+    for 1000 episodes, its MPC step the tree expansion (Fact 2), robots
+    sharded over ranks (no exchange), lockstep on each rank: one batched
+    launch pair per MPC step of all running episodes.  A timed step = one
+    lockstep MPC step (grids on the host, [3, R x 451] candidates up, the
+    batched expansion, R result records down, the per-robot post-processing);
+    K = --steps caps an episode's calls."""
+    import torch
+    import torch.distributed as dist
+    from diplomjourney_amd import run_math_model as rmm
+    from diplomjourney_amd.distributed import shard_range
+    from diplomjourney_amd.episode import percentile
+    starts = rmm.draw_starts(wl["robots"], seed=20261015)
+    lo, hi = shard_range(len(starts), rank, world)
+    rmm.run_tree_batched(starts[lo:hi], max_calls=max(1, args.warmup), integrator=args.integrator,
+                         engine=eng)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st = {}
+    outs = rmm.run_tree_batched(starts[lo:hi], max_calls=args.steps, integrator=args.integrator,
+                                engine=eng, stats=st)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    calls = sum(len(r) for r, _ in outs)
+    lockstep = st["steps"]
+    cands = st["candidates"]      # each call's |V| x |B| (the padding is not counted)
+    t = torch.tensor([elapsed, calls, cands, lockstep], dtype=torch.float64, device=eng.device)
+    if world > 1:
+        mx = t[[0, 3]].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed, lockstep = float(mx[0]), int(mx[1])
+        calls, cands = float(t[1]), float(t[2])
+    stops = {}
+    for _, st in outs:
+        stops[st] = stops.get(st, 0) + 1
+    out = {
+        "metric": METRIC, "value": cands / elapsed, "unit": "rollouts/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / lockstep * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (the script's seeded start/target draws)",
+        "config": {"workload": wl["desc"], "n_steps": 3, "episodes": wl["robots"],
+                   "mpc_calls": calls, "lockstep_steps": lockstep,
+                   "integrator": args.integrator, "episode_stops_rank0": stops,
+                   "parallelism": f"robot-sharded x{world}, no exchange"},
+        "episodes_per_s": wl["robots"] / elapsed,
+        "p50_ms": None,
+        "p50_note": "ms_per_step = one lockstep MPC step of every running episode",
+        "roofline": None, "cpu_baseline": cpu,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -64,6 +64,13 @@ class MpcResult(ctypes.Structure):
                 "traj": self.trajectory()}
 
 
+class MpcCandidate(ctypes.Structure):
+    """mpc_candidate_t: one rank's best candidate (the exchange's payload)."""
+    _fields_ = [("cost", ctypes.c_double), ("index", ctypes.c_int64),
+                ("n_steps", ctypes.c_int32), ("reserved_", ctypes.c_int32),
+                ("v", ctypes.c_double * MPC_MAX_STEPS), ("beta", ctypes.c_double * MPC_MAX_STEPS)]
+
+
 class MpcEpisodeConfig(ctypes.Structure):
     """mpc_episode_config_t: the device-resident math_mpc loop's constants."""
     _fields_ = [(n, ctypes.c_double) for n in (
@@ -113,6 +120,7 @@ class MpcFulltreeResult(ctypes.Structure):
 
 
 RESULT_BYTES = ctypes.sizeof(MpcResult)
+CANDIDATE_BYTES = ctypes.sizeof(MpcCandidate)
 FT_RESULT_BYTES = ctypes.sizeof(MpcFulltreeResult)
 LOG_BYTES = ctypes.sizeof(MpcEpisodeLog)
 PROBLEM_BYTES = ctypes.sizeof(MpcProblem)

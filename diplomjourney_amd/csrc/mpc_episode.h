@@ -22,6 +22,7 @@
 namespace mpc {
 
 constexpr int kEpMaxGrid = 64;
+constexpr uint32_t kChainSpinLimit = 1u << 17;   // bounded device waits: x ~1-2k cycles, ~0.1 s
 constexpr int kConstsWords = static_cast<int>(sizeof(Consts) / 4);
 constexpr int kPubWords = kConstsWords + 2;   // Consts, then t
 static_assert(sizeof(Consts) % 4 == 0 && kPubWords <= 64, "published words: one wave");
@@ -516,6 +517,151 @@ __device__ inline void advance_from_results(const mpc_episode_config_t& c, Episo
                end_chain ? S->chain_pub : nullptr, kPubWords);
 }
 
+// Multi-GPU chained exchange: the global winner of a step among the gathered
+// per-rank candidates (lexicographic (cost, global index)), re-rolled from its
+// gathered controls with the step's constants (emit_winner: the same
+// operations as the rollout that scored it) into `out`, then the episode
+// update.  Every thread of a block of kFinBlock threads.
+template <int INTEG, int ROT>
+__device__ void advance_from_candidates(const mpc_episode_config_t& c, EpisodeState* S,
+                                        const mpc_candidate_t* __restrict__ g, int n,
+                                        mpc_result_t* __restrict__ out,
+                                        mpc_episode_log_t* __restrict__ log, int cap,
+                                        bool end_chain) {
+  __shared__ uint64_t s_head[kStagedWords];
+  __shared__ mpc_episode_log_t s_log;
+  __shared__ mpc_episode_log_t* s_slot;
+  __shared__ int s_best;
+  __shared__ uint64_t s_bk;
+  if (threadIdx.x < kStagedWords)
+    s_head[threadIdx.x] = reinterpret_cast<const uint64_t*>(&S->h)[threadIdx.x];
+  if (threadIdx.x == 0) {
+    int best = 0;
+    uint64_t bk = ~0ull;
+    int64_t bi = INT64_MAX;
+    for (int r = 0; r < n; ++r) {
+      const uint64_t k = g[r].index < 0 ? ~0ull : cost_key(g[r].cost);
+      const int64_t i = g[r].index < 0 ? INT64_MAX : g[r].index;
+      if (r == 0 || rec_less(k, i, bk, bi)) {
+        best = r;
+        bk = k;
+        bi = i;
+      }
+    }
+    s_best = best;
+    s_bk = bk;
+  }
+  __syncthreads();
+  const mpc_candidate_t* w = &g[s_best];
+  const EpisodeHead* Hs = reinterpret_cast<const EpisodeHead*>(s_head);
+  const Consts K = Hs->K;                // the step's constants (before the update)
+  Winner win;
+  emit_winner<INTEG, ROT>(K, nullptr, nullptr, 0, w->n_steps, s_bk, 0, w->index, Hs->incumbent,
+                          out, &win, w->v, w->beta);
+  if (threadIdx.x == 0) {   // emit_winner ended with a barrier; lane 0 holds `win`
+    EpisodeHead H;
+    __builtin_memcpy(&H, s_head, sizeof(EpisodeHead));
+    s_slot = log_slot(log, cap, H.step);
+    episode_advance(c, H, *reinterpret_cast<StaleTraj*>(&s_head[kHeadWords]), win, s_log);
+    __builtin_memcpy(s_head, &H, sizeof(EpisodeHead));
+  }
+  __syncthreads();
+  store_update(&S->h, s_head, s_slot, reinterpret_cast<const uint64_t*>(&s_log),
+               end_chain ? S->chain_pub : nullptr, kPubWords);
+}
+
+template <int INTEG, int ROT>
+__global__ __launch_bounds__(kFinBlock) void k_episode_advance_cand(
+    mpc_episode_config_t c, EpisodeState* __restrict__ S, const mpc_candidate_t* __restrict__ g,
+    int n, mpc_result_t* __restrict__ out, mpc_episode_log_t* __restrict__ log, int cap) {
+  advance_from_candidates<INTEG, ROT>(c, S, g, n, out, log, cap, true);
+}
+
+// A tile block's record in an exchange step: ONE 16-B `sc1` store {cost key,
+// (epoch << 32) | local index} — a data-tagged granule that block 0 of the
+// same launch polls for (no counter, no wait in the tile block).  No
+// candidate: index 0xffffffff.
+__device__ __forceinline__ void store_tagged_rec(Rec* dst, uint64_t key, int64_t idx,
+                                                 uint32_t epoch) {
+  const uint64_t lo = idx == INT64_MAX ? 0xffffffffull
+                                       : static_cast<uint64_t>(static_cast<uint32_t>(idx));
+  asm volatile("global_store_dwordx4 %0, %1, off sc1"
+               :
+               : "v"(dst), "v"(u64x2{key, (static_cast<uint64_t>(epoch) << 32) | lo})
+               : "memory");
+}
+
+// Block 0 of an exchange step, after publishing: wait until every tile
+// block's record of THIS launch has landed (tags == epoch; `sc1` loads, a
+// bounded poll), reduce them and write this rank's best candidate — its
+// (cost, global index) and its controls, one step per lane — to `out`.
+__device__ void collect_local_candidate(const Rec* __restrict__ part, int n_part, uint32_t epoch,
+                                        const double* __restrict__ v,
+                                        const double* __restrict__ b, int64_t n_cand,
+                                        int n_steps, int64_t index_base,
+                                        mpc_candidate_t* __restrict__ out, uint32_t* err) {
+  static_assert(kMaxBlocks <= 8 * kBlock, "eight records per thread");
+  const Rec* ptr[8];
+  u64x2 r[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int p = threadIdx.x + q * kBlock;
+    ptr[q] = part + (p < n_part ? p : n_part - 1);
+  }
+  bool timed_out = false;
+  for (uint32_t it = 0;; ++it) {
+    load8_rec_sc1(ptr, r);
+    bool ok = true;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (threadIdx.x + q * kBlock < n_part)
+        ok = ok && static_cast<uint32_t>(r[q].y >> 32) == epoch;
+    if (__syncthreads_and(ok)) break;
+    if (it >= kChainSpinLimit) {   // uniform: every thread counts the same passes
+      timed_out = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(16);
+  }
+  uint64_t k = ~0ull;
+  int64_t i = INT64_MAX;
+  if (!timed_out) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint32_t lo = static_cast<uint32_t>(r[q].y);
+      const int64_t idx = lo == 0xffffffffu ? INT64_MAX : static_cast<int64_t>(lo);
+      if (threadIdx.x + q * kBlock < n_part && rec_less(r[q].x, idx, k, i)) {
+        k = r[q].x;
+        i = idx;
+      }
+    }
+  } else if (threadIdx.x == 0) {
+    *err = 3u;
+  }
+  block_argmin(k, i);
+  __shared__ uint64_t s_k;
+  __shared__ int64_t s_i;
+  if (threadIdx.x == 0) {
+    s_k = k;
+    s_i = i;
+  }
+  __syncthreads();
+  k = s_k;
+  i = s_i;
+  const bool valid = k != ~0ull;
+  const int q = threadIdx.x;
+  if (q < MPC_MAX_STEPS) {   // one value per lane
+    out->v[q] = (valid && q < n_steps) ? v[q * n_cand + i] : 0.0;
+    out->beta[q] = (valid && q < n_steps) ? b[q * n_cand + i] : 0.0;
+  }
+  if (q == 0) {
+    out->cost = valid ? key_cost(k) : __builtin_inf();
+    out->index = valid ? index_base + i : -1;
+    out->n_steps = n_steps;
+    out->reserved_ = 0;
+  }
+}
+
 __global__ __launch_bounds__(64) void k_episode_advance(mpc_episode_config_t c,
                                                         EpisodeState* __restrict__ S,
                                                         const mpc_result_t* __restrict__ res,
@@ -528,9 +674,11 @@ __global__ __launch_bounds__(64) void k_episode_advance(mpc_episode_config_t c,
 // Chained episode step (heading mode kRotCum): ONE launch = this step's
 // streaming rollout + the completion of the PREVIOUS step.  Block 0 completes
 // step k-1 — kChainFin (one GPU): k_finalize's record reduction, winner
-// re-roll and episode update; kChainAdv (multi-GPU): k_episode_advance's
-// selection over the gathered per-rank winners and the update — and publishes
-// step k's constants as epoch-tagged words (EpisodeState::chain_pub).
+// re-roll and episode update; kChainXchg (multi-GPU): the selection over the
+// gathered per-rank candidates, the winner's re-roll and the update — and
+// publishes step k's constants as epoch-tagged words (EpisodeState::chain_pub);
+// kChainXchg's block 0 then collects this launch's tagged block records into
+// the rank's candidate (collect_local_candidate), which the caller gathers.
 // The other blocks do not wait for it: in kRotCum mode a candidate's rollout
 // needs no start pose, only the step size h (and the constant wheelbase
 // terms).  A block reads the published words once, right after its first
@@ -545,8 +693,7 @@ __global__ __launch_bounds__(64) void k_episode_advance(mpc_episode_config_t c,
 // carry different epochs and the update that ends a chain (k_finalize's hook,
 // k_episode_advance) clears the tags.  The wait is bounded: if the words
 // never came, chain_error is set instead of hanging the GPU.
-constexpr int kChainFin = 1, kChainAdv = 2;
-constexpr uint32_t kChainSpinLimit = 1u << 17;   // x ~2k cycles: ~0.1 s
+constexpr int kChainFin = 1, kChainXchg = 3;
 
 // LDS dwords (Consts layout) -> wave-uniform Consts, field by field (no
 // memory view of the struct: it stays in SGPRs).
@@ -627,7 +774,7 @@ __global__ __launch_bounds__(kBlock, kChainWaves) void k_episode_chain(
     const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part,
     int has_prev, const Rec* __restrict__ part_prev, int n_part_prev,
     const double* __restrict__ v_prev, const double* __restrict__ b_prev, int64_t index_base,
-    mpc_result_t* __restrict__ out_prev, const mpc_result_t* __restrict__ gathered,
+    mpc_result_t* __restrict__ out_prev, const mpc_candidate_t* __restrict__ gathered,
     int n_gathered, mpc_episode_config_t ecfg, mpc_episode_log_t* __restrict__ log, int cap) {
   static_assert(ROT == kRotCum, "chained steps need the pose-independent recurrence");
   if (blockIdx.x == 0) {
@@ -639,7 +786,8 @@ __global__ __launch_bounds__(kBlock, kChainWaves) void k_episode_chain(
                                                         b_prev, n_cand, n_steps, index_base,
                                                         S->h.incumbent, out_prev, ecfg, hook);
       } else {
-        advance_from_results(ecfg, S, gathered, n_gathered, log, cap, false);
+        advance_from_candidates<INTEG, ROT>(ecfg, S, gathered, n_gathered, out_prev, log, cap,
+                                            false);
       }
     }
     chain_publish(S, epoch);
@@ -649,6 +797,12 @@ __global__ __launch_bounds__(kBlock, kChainWaves) void k_episode_chain(
     // wrong form: flag it (chain_error = 2) instead of returning wrong costs
     // silently.  (chain_publish ended with a barrier after the head store.)
     if (threadIdx.x == 0 && (S->h.K.L_pow2 != 0) != PL2) S->chain_error = 2u;
+    // kChainXchg passes the rank's candidate record in part_prev's slot (one
+    // kernel argument fewer: a further SGPR pair spilled a VGPR)
+    if constexpr (MODE == kChainXchg)
+      collect_local_candidate(part, gridDim.x - 1, epoch, v, b, n_cand, n_steps, index_base,
+                              reinterpret_cast<mpc_candidate_t*>(const_cast<Rec*>(part_prev)),
+                              &S->chain_error);
     return;
   }
   constexpr int CPL = 2;
@@ -748,7 +902,12 @@ __global__ __launch_bounds__(kBlock, kChainWaves) void k_episode_chain(
     }
   }
   block_argmin(best_k, best_i);
-  if (threadIdx.x == 0) part[blockIdx.x - 1] = Rec{best_k, best_i};
+  if (threadIdx.x == 0) {
+    if constexpr (MODE == kChainXchg)
+      store_tagged_rec(&part[blockIdx.x - 1], best_k, best_i, epoch);
+    else
+      part[blockIdx.x - 1] = Rec{best_k, best_i};
+  }
 }
 
 }  // namespace mpc

@@ -536,21 +536,19 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
                            const double* beta_prev, mpc_result_t* out_prev,
                            const mpc_result_t* gathered, int32_t n_gathered,
                            mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream) {
+  (void)gathered;
+  (void)n_gathered;
   if (check_episode_cfg(cfg) != MPC_OK ||
       check_episode_arrays(state, v_sc, beta_sc, n_cand, n_steps) != MPC_OK || index_base < 0 ||
-      log_capacity < 0 || (mode != MPC_CHAIN_FINALIZE && mode != MPC_CHAIN_ADVANCE) || epoch == 0)
+      log_capacity < 0 || mode != MPC_CHAIN_FINALIZE || epoch == 0)
     return MPC_ERR_ARG;
   if (mode_ok(integrator) != MPC_OK || !is_cum(integrator) || !wide_ok(v_sc, beta_sc, n_cand))
     return MPC_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
   int has_prev = 0;
-  if (mode == MPC_CHAIN_FINALIZE && v_prev) {
+  if (v_prev) {
     if (!beta_prev || !out_prev || !ws_prev || !wide_ok(v_prev, beta_prev, n_cand))
       return MPC_ERR_ARG;
-    has_prev = 1;
-  }
-  if (mode == MPC_CHAIN_ADVANCE && gathered) {
-    if (n_gathered < 1) return MPC_ERR_ARG;
     has_prev = 1;
   }
   EpisodeState* S = static_cast<EpisodeState*>(state);
@@ -562,20 +560,64 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
   constexpr int I = MPC_INTEG_RECT;
   auto launch = [&](auto pl2_tag) {
     constexpr bool P = decltype(pl2_tag)::value;
-    if (mode == MPC_CHAIN_FINALIZE)
-      k_episode_chain<I, kRotCum, kChainFin, P><<<grid, kBlock, 0, st>>>(
-          S, epoch, v_sc, beta_sc, n_cand, n_steps, static_cast<Rec*>(ws), has_prev,
-          static_cast<const Rec*>(ws_prev), n_part_prev, v_prev, beta_prev, index_base, out_prev,
-          nullptr, 0, *cfg, log, log_capacity);
-    else
-      k_episode_chain<I, kRotCum, kChainAdv, P><<<grid, kBlock, 0, st>>>(
-          S, epoch, v_sc, beta_sc, n_cand, n_steps, static_cast<Rec*>(ws), has_prev, nullptr, 0,
-          nullptr, nullptr, index_base, nullptr, gathered, n_gathered, *cfg, log, log_capacity);
+    k_episode_chain<I, kRotCum, kChainFin, P><<<grid, kBlock, 0, st>>>(
+        S, epoch, v_sc, beta_sc, n_cand, n_steps, static_cast<Rec*>(ws), has_prev,
+        static_cast<const Rec*>(ws_prev), n_part_prev, v_prev, beta_prev, index_base, out_prev,
+        nullptr, 0, *cfg, log, log_capacity);
   };
   if (pl2)
     launch(std::true_type{});
   else
     launch(std::false_type{});
+  return last_hip_status();
+}
+
+int mpc_episode_exchange_step(const mpc_episode_config_t* cfg, void* state, uint32_t epoch,
+                              const double* v_sc, const double* beta_sc, int64_t n_cand,
+                              int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
+                              size_t ws_bytes, const mpc_candidate_t* gathered,
+                              int32_t n_gathered, mpc_result_t* out_prev, mpc_candidate_t* local,
+                              mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream) {
+  if (check_episode_cfg(cfg) != MPC_OK ||
+      check_episode_arrays(state, v_sc, beta_sc, n_cand, n_steps) != MPC_OK || index_base < 0 ||
+      log_capacity < 0 || epoch == 0 || !local || !out_prev)
+    return MPC_ERR_ARG;
+  // local indices travel in the low 32 bits of a tagged record
+  if (n_cand > 0x7fffffffll || (gathered && n_gathered < 1)) return MPC_ERR_ARG;
+  if (mode_ok(integrator) != MPC_OK || !is_cum(integrator) || !wide_ok(v_sc, beta_sc, n_cand))
+    return MPC_ERR_UNSUPPORTED;
+  if (!ws || ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
+  EpisodeState* S = static_cast<EpisodeState*>(state);
+  int e;
+  const int pl2 = frexp(cfg->L, &e) == 0.5 ? 1 : 0;
+  const int64_t grid = rollout_grid<kCplWide>(n_cand) + 1;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  constexpr int I = MPC_INTEG_RECT;
+  auto launch = [&](auto pl2_tag) {
+    constexpr bool P = decltype(pl2_tag)::value;
+    k_episode_chain<I, kRotCum, kChainXchg, P><<<grid, kBlock, 0, st>>>(
+        S, epoch, v_sc, beta_sc, n_cand, n_steps, static_cast<Rec*>(ws), gathered ? 1 : 0,
+        reinterpret_cast<const Rec*>(local), 0, nullptr, nullptr, index_base, out_prev, gathered,
+        n_gathered, *cfg, log, log_capacity);
+  };
+  if (pl2)
+    launch(std::true_type{});
+  else
+    launch(std::false_type{});
+  return last_hip_status();
+}
+
+int mpc_episode_exchange_flush(const mpc_episode_config_t* cfg, void* state, int32_t integrator,
+                               const mpc_candidate_t* gathered, int32_t n_gathered,
+                               mpc_result_t* out, mpc_episode_log_t* log, int32_t log_capacity,
+                               mpc_stream_t stream) {
+  if (check_episode_cfg(cfg) != MPC_OK || !state || !gathered || n_gathered < 1 || !out ||
+      log_capacity < 0)
+    return MPC_ERR_ARG;
+  if (mode_ok(integrator) != MPC_OK || !is_cum(integrator)) return MPC_ERR_UNSUPPORTED;
+  k_episode_advance_cand<MPC_INTEG_RECT, kRotCum>
+      <<<1, kFinBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+          *cfg, static_cast<EpisodeState*>(state), gathered, n_gathered, out, log, log_capacity);
   return last_hip_status();
 }
 

@@ -25,10 +25,10 @@ import time
 import torch
 
 from . import math_model_tree as mmt
-from .abi import (LOG_BYTES, MPC_EP_ARRIVED, MPC_EP_BREAK, MPC_EP_EVENT, MPC_EP_LIMIT,
-                  MPC_EP_STALE, MPC_EP_STUCK, RESULT_BYTES, MpcEpisodeConfig, MpcEpisodeLog,
-                  make_problem)
-from .distributed import exchange_winner, gather_results, shard_range
+from .abi import (CANDIDATE_BYTES, LOG_BYTES, MPC_EP_ARRIVED, MPC_EP_BREAK, MPC_EP_EVENT,
+                  MPC_EP_LIMIT, MPC_EP_STALE, MPC_EP_STUCK, RESULT_BYTES, MpcEpisodeConfig,
+                  MpcEpisodeLog, make_problem)
+from .distributed import exchange_winner, gather_bytes, gather_results, shard_range
 from . import native
 
 
@@ -263,6 +263,9 @@ class DeviceEpisode:
         # flush() completes the last one.
         self.chain = bool(chain)
         self._ws = [self.ws, torch.empty_like(self.ws)] if self.chain else [self.ws]
+        # exchange + chain: this rank's best candidate of the step (the
+        # all_gather payload of mpc_episode_exchange_step)
+        self.cand = torch.zeros(CANDIDATE_BYTES, dtype=torch.uint8, device=dev)
         # generate: steps without caller controls draw their candidates inside
         # the rollout (mpc_episode_generate_step) instead of sampling them into
         # v_sc / b_sc first — the same candidates, never written to HBM
@@ -322,18 +325,17 @@ class DeviceEpisode:
                 self.log.data_ptr(), self.log_capacity, st), "mpc_episode_chain_step")
             self._pending = (v, b)
         else:
-            native.check(L.mpc_episode_chain_step(
-                ctypes.byref(self.cfg), self.state.data_ptr(), 2, self._next_epoch(),
-                v.data_ptr(), b.data_ptr(),
-                self.n_local, self.n_steps, self.lo, self._integ, ws.data_ptr(),
-                ws_prev.data_ptr(), ws.numel(), None, None, None,
-                pend.data_ptr() if pend is not None else None, self.world if pend is not None
-                else 0, self.log.data_ptr(), self.log_capacity, st), "mpc_episode_chain_step")
-            native.check(L.mpc_episode_finalize(
-                self.state.data_ptr(), v.data_ptr(), b.data_ptr(), self.n_local, self.n_steps,
-                self.lo, self._integ, ws.data_ptr(), ws.numel(), self.local.data_ptr(), None,
-                None, 0, st), "mpc_episode_finalize")
-            self._pending = gather_results(self.local, self.group)
+            # one launch (selection of step k-1 over the gathered candidates +
+            # the rollout of step k + this rank's candidate), then ONE
+            # all_gather of the 536-B candidates
+            native.check(L.mpc_episode_exchange_step(
+                ctypes.byref(self.cfg), self.state.data_ptr(), self._next_epoch(),
+                v.data_ptr(), b.data_ptr(), self.n_local, self.n_steps, self.lo, self._integ,
+                ws.data_ptr(), ws.numel(), pend.data_ptr() if pend is not None else None,
+                self.world if pend is not None else 0, self.winner.data_ptr(),
+                self.cand.data_ptr(), self.log.data_ptr(), self.log_capacity, st),
+                "mpc_episode_exchange_step")
+            self._pending = gather_bytes(self.cand, self.group)
         if events:
             events[1].record()
         if pend is not None:
@@ -358,9 +360,10 @@ class DeviceEpisode:
                 self.local.data_ptr(), ctypes.byref(self.cfg), self.log.data_ptr(),
                 self.log_capacity, st), "mpc_episode_finalize")
         else:
-            native.check(L.mpc_episode_advance(
-                ctypes.byref(self.cfg), self.state.data_ptr(), pend.data_ptr(), self.world,
-                self.log.data_ptr(), self.log_capacity, st), "mpc_episode_advance")
+            native.check(L.mpc_episode_exchange_flush(
+                ctypes.byref(self.cfg), self.state.data_ptr(), self._integ, pend.data_ptr(),
+                self.world, self.winner.data_ptr(), self.log.data_ptr(), self.log_capacity, st),
+                "mpc_episode_exchange_flush")
         self.steps_enqueued += 1
 
     def chain_error(self):

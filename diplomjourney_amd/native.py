@@ -32,7 +32,7 @@ EXPORTS = (
     "mpc_sample_controls", "mpc_episode_state_bytes", "mpc_episode_reset",
     "mpc_episode_expand", "mpc_episode_advance", "mpc_episode_sample", "mpc_episode_partials",
     "mpc_episode_finalize", "mpc_episode_rollout", "mpc_episode_step", "mpc_episode_chain_step",
-    "mpc_episode_chain_error",
+    "mpc_episode_chain_error", "mpc_episode_exchange_step", "mpc_episode_exchange_flush",
     "mpc_episode_generate_workspace_bytes", "mpc_episode_generate_step",
     "mpc_fulltree_workspace_bytes", "mpc_fulltree_argmin",
     "mpc_fulltree_batched_workspace_bytes", "mpc_fulltree_argmin_batched",
@@ -147,6 +147,13 @@ def lib():
                                          ctypes.c_uint32, _P, _P,
                                          _I64, _I32, _I64, _I32, _P, _P, ctypes.c_size_t, _P,
                                          _P, _P, _P, _I32, _P, _I32, _P]
+    L.mpc_episode_exchange_step.restype = ctypes.c_int
+    L.mpc_episode_exchange_step.argtypes = [ctypes.POINTER(MpcEpisodeConfig), _P, ctypes.c_uint32,
+                                            _P, _P, _I64, _I32, _I64, _I32, _P, ctypes.c_size_t,
+                                            _P, _I32, _P, _P, _P, _I32, _P]
+    L.mpc_episode_exchange_flush.restype = ctypes.c_int
+    L.mpc_episode_exchange_flush.argtypes = [ctypes.POINTER(MpcEpisodeConfig), _P, _I32, _P, _I32,
+                                             _P, _P, _I32, _P]
     L.mpc_episode_chain_error.restype = ctypes.c_int
     L.mpc_episode_chain_error.argtypes = [_P, ctypes.POINTER(_I32), _P]
     L.mpc_episode_generate_workspace_bytes.restype = ctypes.c_size_t

@@ -295,6 +295,189 @@ def is_on_target_of(r):
     return (r.x_t - r.x) ** 2 + (r.y_t - r.y) ** 2 <= eps
 
 
-__all__ = ["configure", "shard_over", "draw_starts", "run_batched", "is_on_target", "get_distance_from_line", "get_distance_from_target",
-           "saturation", "control_criterion", "predictive_control", "start_episode",
-           "run_episode", "prediction_horizon"]
+# ----------------------------------------------------------------------------
+# The script's episode loop over the tree expansion (SURVEY §8b "entry", Fact
+# 2): at config.py's resolution the full tree above cannot run (S1^3 = 1.4e13
+# leaves, MemoryError in the reference), so the named entry drives
+# math_model_tree.py's MPC step instead — the acceleration-limited grid
+# around the current (v, beta) (:239-256, <= 11 x 41 controls), N = 3 constant
+# sequences, strict-< first minimum, the incumbent reset to sys.maxsize after
+# every call (:428), the finishing logic m (:392-414) — inside the episode
+# loop of run_math_model.py:231-280 (five uniform draws per episode,
+# is_on_target, the two-non-move stop).  Per episode the script resets t, v
+# and the incumbent (:233-234, :252); m, steps_for_slowing, optimal_trajectory
+# and beta are reset too here, so that episodes are independent and can run
+# side by side (the script leaks them from one episode into the next).
+
+TREE_CAND = 11 * 41        # the largest acceleration-limited grid (:239-256)
+
+
+def _tree_globals(start):
+    from . import math_model_tree as mmt
+    x0, y0, phi0, xt, yt = start
+    mmt.t = 0
+    mmt.m = 0
+    mmt.steps_for_slowing = 0
+    mmt.x_t, mmt.y_t, mmt.x_0, mmt.y_0, mmt.phi_0 = xt, yt, x0, y0, phi0
+    mmt.optimal_trajectory = [[[0]]]
+    mmt.optimal_criterion = mmt.control_criterion([x0, y0, phi0])      # :252
+    return mmt
+
+
+def run_tree_episode(start, max_calls=None):
+    """One episode of the script's loop (:231-280) whose MPC step is the drop-in
+    math_model_tree.predictive_control (one C-ABI expansion per call).
+    start = (x_0, y_0, phi_0, x_t, y_t) as draw_starts() draws them.
+    Returns (list of returned [x, y, phi, v, beta], stop)."""
+    mmt = _tree_globals(start)
+    x0, y0, phi0, xt, yt = start
+    x, y, phi, v, b = x0, y0, phi0, 0, 0
+    k = 0
+    x_previous, y_previous = x, y
+    records = []
+    while not is_on_target(x, y, xt, yt):
+        if max_calls is not None and len(records) == max_calls:
+            return records, "max_calls"
+        c = mmt.predictive_control(x, y, phi, xt, yt, mmt.vector_of_velocities(v),
+                                   mmt.vector_of_beta_angles(b), False)
+        records.append(list(c))
+        x, y, phi, v, b = c
+        if x == x_previous and y == y_previous:
+            k += 1
+        if k == 2:
+            return records, "recursive_error"
+        x_previous, y_previous = x, y
+    return records, "on_target"
+
+
+def _tree_grids(v, b):
+    """vector_of_velocities / vector_of_beta_angles (:239-256) of R robots at
+    once (numpy float64, the same operations in the same order), compacted,
+    and the reference's enumeration k = a |B| + b over them padded to
+    TREE_CAND with NaN controls.  Returns (v_cand, b_cand) [R, TREE_CAND]."""
+    from . import math_model_tree as mmt
+    R = len(v)
+    rv = (mmt.v_acc_max * mmt.delta_t) / mmt.delta_v
+    iv = np.arange(1 + 2 * int(rv), dtype=np.float64)
+    cv = v[:, None] + mmt.delta_v * (iv[None, :] - rv)
+    okv = ~(cv < 0) & (cv < mmt.v_max)
+    rb = (math.degrees(mmt.beta_acc_max) * mmt.delta_t) / math.degrees(mmt.delta_beta)
+    ib = np.arange(1 + 2 * int(rb), dtype=np.float64)
+    cb = b[:, None] + mmt.delta_beta * (ib[None, :] - rb)
+    okb = np.abs(cb) <= mmt.beta_max + math.radians(mmt.eps_beta)
+    # compaction: accepted entries first, in order (stable sort on "rejected")
+    ov = np.argsort(~okv, axis=1, kind="stable")
+    ob = np.argsort(~okb, axis=1, kind="stable")
+    Vc = np.take_along_axis(cv, ov, axis=1)
+    Bc = np.take_along_axis(cb, ob, axis=1)
+    nv = okv.sum(axis=1)
+    nb = okb.sum(axis=1)
+    k = np.arange(TREE_CAND)[None, :]
+    nbk = np.maximum(nb, 1)[:, None]
+    a = np.minimum(k // nbk, Vc.shape[1] - 1)
+    bb = k % nbk
+    valid = k < (nv * nb)[:, None]
+    rows = np.arange(R)[:, None]
+    vc = np.where(valid, Vc[rows, a], np.nan)
+    bc = np.where(valid, Bc[rows, bb], np.nan)
+    return vc, bc
+
+
+class _TreeRobot:
+    """One episode of the tree-expansion loop (the module globals of
+    math_model_tree.py and run_math_model.py, per robot)."""
+
+    def __init__(self, start):
+        from . import math_model_tree as mmt
+        self.x_0, self.y_0, self.phi_0, self.x_t, self.y_t = start
+        self.x, self.y, self.phi, self.v, self.beta = self.x_0, self.y_0, self.phi_0, 0.0, 0.0
+        saved = (mmt.x_t, mmt.y_t, mmt.x_0, mmt.y_0)
+        mmt.x_t, mmt.y_t, mmt.x_0, mmt.y_0 = self.x_t, self.y_t, self.x_0, self.y_0
+        self.incumbent = mmt.control_criterion([self.x_0, self.y_0, self.phi_0])   # :252
+        mmt.x_t, mmt.y_t, mmt.x_0, mmt.y_0 = saved
+        self.m = 0
+        self.ot = None            # optimal_trajectory[0] (3 layer states), result_v/beta
+        self.k = 0
+        self.prev = (self.x, self.y)
+        self.records = []
+        self.stop = None
+
+
+def run_tree_batched(starts, max_calls=None, integrator="qk21", engine=None, stats=None):
+    """The tree-expansion episode loop for len(starts) episodes at once, one
+    robot per episode in lockstep: every MPC step of all running episodes is
+    ONE batched launch pair (mpc_rollout_argmin_batched — config E's kernel,
+    robot = blockIdx.y, per-robot problem constants and incumbent on the
+    device) over [3, R x 451] candidate controls (each robot's grid around its
+    own (v, beta), the reference's enumeration, NaN padding), then each
+    robot's post-processing on the host.  Returns [(records, stop)] per
+    episode, as run_tree_episode returns them.  stats (optional dict) receives
+    the lockstep steps and the candidates rolled out (padding excluded)."""
+    from . import math_model_tree as mmt
+    from .abi import make_problem
+    from .expansion import problems_to_device, results_from_device
+    eng = engine or _device()[0]
+    robots = [_TreeRobot(s) for s in starts]
+    t = 0
+    maxsize = float(__import__("sys").maxsize)
+    while True:
+        live = []
+        for r in robots:
+            if r.stop is not None:
+                continue
+            if is_on_target(r.x, r.y, r.x_t, r.y_t):
+                r.stop = "on_target"
+            elif max_calls is not None and len(r.records) == max_calls:
+                r.stop = "max_calls"
+            else:
+                live.append(r)
+        if not live:
+            break
+        t += delta_t                                                # :302
+        R = len(live)
+        vc, bc = _tree_grids(np.array([r.v for r in live], dtype=np.float64),
+                             np.array([r.beta for r in live], dtype=np.float64))
+        if stats is not None:
+            stats["steps"] = stats.get("steps", 0) + 1
+            stats["candidates"] = stats.get("candidates", 0) + int((~np.isnan(vc)).sum())
+        v_sc = torch.from_numpy(np.ascontiguousarray(vc.reshape(1, -1))).to(eng.device)
+        b_sc = torch.from_numpy(np.ascontiguousarray(bc.reshape(1, -1))).to(eng.device)
+        v_sc = v_sc.expand(3, -1).contiguous()
+        b_sc = b_sc.expand(3, -1).contiguous()
+        probs = problems_to_device([make_problem(r.x, r.y, r.phi, r.x_t, r.y_t, r.x_0, r.y_0, L,
+                                                 t, t + delta_t) for r in live], eng.device)
+        inc = torch.tensor([r.incumbent for r in live], dtype=torch.float64, device=eng.device)
+        res = results_from_device(eng.rollout_argmin_batched(probs, v_sc, b_sc, TREE_CAND,
+                                                             incumbents_dev=inc,
+                                                             integrator=integrator))
+        for r, w in zip(live, res):
+            if w.found:                                             # :351-359
+                tr = w.trajectory()
+                r.ot = ([list(tr[0]), list(tr[1]), list(tr[2])], w.v, w.beta)
+            if r.ot is None:
+                raise TypeError("'int' object is not subscriptable")   # [[[0]]], as the script
+            r.incumbent = maxsize                                   # :428
+            ot, rv, rb = r.ot
+            kk = 0                                                  # :392-414
+            if r.m == 2:
+                kk = 2
+            elif r.m == 1:
+                kk = 1
+                r.m += 1
+            elif mmt.is_on_target(ot[2][0], ot[2][1], r.x_t, r.y_t)[0]:
+                r.m += 1
+            c = [ot[kk][0], ot[kk][1], ot[kk][2], rv, rb]
+            r.records.append(c)
+            r.x, r.y, r.phi, r.v, r.beta = c
+            if r.x == r.prev[0] and r.y == r.prev[1]:             # :268-272
+                r.k += 1
+            if r.k == 2:
+                r.stop = "recursive_error"
+            r.prev = (r.x, r.y)
+    return [(r.records, r.stop) for r in robots]
+
+
+__all__ = ["configure", "shard_over", "draw_starts", "run_batched", "is_on_target",
+           "get_distance_from_line", "get_distance_from_target", "saturation", "control_criterion",
+           "predictive_control", "start_episode", "run_episode", "prediction_horizon",
+           "run_tree_episode", "run_tree_batched"]

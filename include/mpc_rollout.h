@@ -76,6 +76,17 @@ typedef struct mpc_problem {
 
 /* The selected candidate.  `found` == 0 means no candidate beat `incumbent`
  * (strict <, :351): the caller keeps its stale trajectory. */
+/* One rank's best candidate of a sharded MPC step, as the multi-GPU exchange
+ * gathers it: the arg-min's (cost, global index) and the candidate's
+ * controls, so that whichever rank holds the global winner, every rank can
+ * re-roll it (mpc_episode_exchange_step).  536 B. */
+typedef struct mpc_candidate {
+  double cost;                      /* +inf when the shard has no finite cost  */
+  int64_t index;                    /* global index, -1 when none              */
+  int32_t n_steps, reserved_;
+  double v[MPC_MAX_STEPS], beta[MPC_MAX_STEPS];   /* its controls, per step  */
+} mpc_candidate_t;
+
 typedef struct mpc_result {
   double cost;                      /* control_criterion of the winner         */
   int64_t index;                    /* global index, -1 when no finite cost    */
@@ -263,28 +274,22 @@ int mpc_episode_step(void* state, const double* v_sc, const double* beta_sc, int
                      size_t ws_bytes, mpc_result_t* out, const mpc_episode_config_t* advance,
                      mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
 
-/* Chained step (integrator MPC_INTEG_RECT | MPC_HEADING_CUMULATIVE): ONE
- * launch = the streaming rollout of this step (v_sc / beta_sc, records into
- * ws) + the selection that completes the PREVIOUS step, run by the launch's
+/* Chained step (integrator MPC_INTEG_RECT | MPC_HEADING_CUMULATIVE, one GPU):
+ * ONE launch = the streaming rollout of this step (v_sc / beta_sc, records
+ * into ws) + the selection that completes the PREVIOUS step — its records
+ * (ws_prev), controls (v_prev / beta_prev; NULL = no previous step) -> winner
+ * re-rolled into out_prev, episode update (cfg, log) — run by the launch's
  * first block while the other blocks roll out (they need its published
- * constants only for the final pose transform and the criterion):
- *   mode MPC_CHAIN_FINALIZE (one GPU): the previous step's records (ws_prev),
- *        controls (v_prev / beta_prev; NULL = no previous step) -> winner re-
- *        rolled into out_prev, episode update (cfg, log);
- *   mode MPC_CHAIN_ADVANCE (multi-GPU): selection over the previous step's
- *        gathered per-rank winners (gathered, n_gathered; NULL = none) and the
- *        update; the local winner of THIS step still needs
- *        mpc_episode_finalize (advance = NULL) before the all_gather.
- * The last step of a chain is completed by mpc_episode_finalize (one GPU) or
- * mpc_episode_advance (multi-GPU); either ends the chain.  epoch: nonzero,
- * different from the previous chained launch's.  Aligned path only (n_cand
- * even, 16-B aligned controls): MPC_ERR_UNSUPPORTED otherwise.  ws / ws_prev:
- * two workspaces of mpc_workspace_bytes(n_cand, n_steps) each, alternated.
- * cfg must be the configuration the state was reset with: the launch picks
- * its wheelbase form (L a power of two or not) from cfg->L, the rollout uses
- * the state's constants; a mismatch sets chain error 2 (mpc_episode_chain_error). */
+ * constants only for the final pose transform and the criterion).
+ * The last step of a chain is completed by mpc_episode_finalize, which ends
+ * the chain.  mode: MPC_CHAIN_FINALIZE.  epoch: nonzero, different from the
+ * previous chained launch's.  Aligned path only (n_cand even, 16-B aligned
+ * controls): MPC_ERR_UNSUPPORTED otherwise.  ws / ws_prev: two workspaces of
+ * mpc_workspace_bytes(n_cand, n_steps) each, alternated.  cfg must be the
+ * configuration the state was reset with: the launch picks its wheelbase form
+ * (L a power of two or not) from cfg->L, the rollout uses the state's
+ * constants; a mismatch sets chain error 2 (mpc_episode_chain_error). */
 #define MPC_CHAIN_FINALIZE 1
-#define MPC_CHAIN_ADVANCE 2
 int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t mode,
                            uint32_t epoch, const double* v_sc, const double* beta_sc,
                            int64_t n_cand,
@@ -293,6 +298,31 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
                            const double* beta_prev, mpc_result_t* out_prev,
                            const mpc_result_t* gathered, int32_t n_gathered,
                            mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
+/* Multi-GPU chained step (same integrator and alignment rules): ONE launch per
+ * rank and MPC step, then ONE all_gather of `local` (sizeof(mpc_candidate_t)
+ * per rank) by the caller — the all-reduce(min+index) of SURVEY §8e:
+ *   block 0: the lexicographic (cost, global index) minimum of the previous
+ *            step's gathered per-rank candidates (NULL = no previous step),
+ *            re-rolled from its gathered controls into out_prev (the global
+ *            winner, on every rank), the episode update, this step's
+ *            constants published; then it collects this launch's block
+ *            records (epoch-tagged 16-B granules, no counter) and writes this
+ *            rank's best candidate (cost, global index, controls) to `local`;
+ *   other blocks: the rollout of this rank's shard (index_base).
+ * ws: mpc_workspace_bytes(n_cand, n_steps) (one; consecutive launches are
+ * stream-ordered).  The last step is completed by mpc_episode_exchange_flush
+ * over its gathered candidates, which ends the chain.  A collection that
+ * timed out sets chain error 3. */
+int mpc_episode_exchange_step(const mpc_episode_config_t* cfg, void* state, uint32_t epoch,
+                              const double* v_sc, const double* beta_sc, int64_t n_cand,
+                              int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,
+                              size_t ws_bytes, const mpc_candidate_t* gathered,
+                              int32_t n_gathered, mpc_result_t* out_prev, mpc_candidate_t* local,
+                              mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
+int mpc_episode_exchange_flush(const mpc_episode_config_t* cfg, void* state, int32_t integrator,
+                               const mpc_candidate_t* gathered, int32_t n_gathered,
+                               mpc_result_t* out, mpc_episode_log_t* log, int32_t log_capacity,
+                               mpc_stream_t stream);
 /* Generated controls (one GPU): one MPC step of the device-resident episode
  * whose candidates are never materialised — the same candidates, bit for bit,
  * as mpc_episode_sample followed by mpc_episode_step (advance = cfg) on the
@@ -309,7 +339,8 @@ int mpc_episode_generate_step(const mpc_episode_config_t* cfg, void* state, int6
                               int32_t log_capacity, mpc_stream_t stream);
 /* Nonzero if a chained step went wrong: 1 = a chained step's wait for the
  * published constants timed out (the launch then ran on stale constants);
- * 2 = cfg's wheelbase form disagreed with the state's.
+ * 2 = cfg's wheelbase form disagreed with the state's; 3 = an exchange step's
+ * collection of its block records timed out (`local` then holds none).
  * Reads the device state (syncs). */
 int mpc_episode_chain_error(const void* state, int32_t* error, mpc_stream_t stream);
 

@@ -170,3 +170,26 @@ def test_batched_equals_sequential_episodes(engine):
                 assert math.isclose(r["optimal_criterion"], crit, rel_tol=COST_RTOL)
     finally:
         rmm.configure()
+
+
+def test_tree_episode_loop_batched_equals_sequential(engine):
+    """run_math_model.py's episode loop over the tree expansion (the named
+    entry at config.py's resolution, SURVEY Fact 2): R episodes in lockstep
+    through the batched kernel (mpc_rollout_argmin_batched) return, call by
+    call, exactly what R sequential runs of the drop-in predictive_control
+    return (chosen (v, beta) identical, pose within 1e-12), and stop the same
+    way."""
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd import run_math_model as rmm
+    starts = rmm.draw_starts(6, seed=20261015)
+    try:
+        seq = [rmm.run_tree_episode(s, max_calls=120) for s in starts]
+    finally:
+        mmt.reset_state()
+    bat = rmm.run_tree_batched(starts, max_calls=120, integrator="qk21", engine=engine)
+    assert sum(len(r) for r, _ in seq) > 300
+    for (rs, ss), (rb, sb) in zip(seq, bat):
+        assert ss == sb and len(rs) == len(rb)
+        for a, b in zip(rs, rb):
+            assert a[3:] == b[3:]
+            assert max(abs(p - q) for p, q in zip(a[:3], b[:3])) <= 1e-12

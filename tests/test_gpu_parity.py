@@ -225,6 +225,96 @@ def test_sharded_exchange_equals_single_launch(engine):
     assert dev.cost == single.cost and dev.trajectory() == single.trajectory()
 
 
+def test_config_d_full_size_sharded_vs_oracle(engine, oracle):
+    """Config D at its full size on one GPU: N = 12, 1e7 candidates in the 8
+    contiguous shards of 8 ranks (index_base), each shard's winner from the
+    bench's arithmetic (rect+cum), then the device all-reduce(min+index)
+    selection over the 8 records — against the oracle's scan of every shard
+    (reference arithmetic, glibc trig, 8 host threads) and its lexicographic
+    minimum: same global index and control, states within 1e-9."""
+    from concurrent.futures import ThreadPoolExecutor
+    from diplomjourney_amd.abi import RESULT_BYTES, make_problem
+    from diplomjourney_amd.distributed import shard_range
+    n, ns, world = 10_000_000, 12, 8
+    prob = make_problem(-0.3, 0.4, 2.0, 2, 3, 0, 0, 0.5, 1.0, 1.05)
+    gathered = torch.empty(world * RESULT_BYTES, dtype=torch.uint8, device="cuda")
+    futs = []
+    with ThreadPoolExecutor(max_workers=8) as pool:
+        for r in range(world):
+            lo, hi = shard_range(n, r, world)
+            _, _, vs, bs = _sampled(engine, hi - lo, ns, seed=13, base=lo)
+            engine.rollout_argmin(prob, vs, bs, index_base=lo, incumbent=INC_MAX,
+                                  integrator="rect+cum",
+                                  out=gathered[r * RESULT_BYTES:(r + 1) * RESULT_BYTES])
+            vh, bh = vs.cpu().numpy(), bs.cpu().numpy()
+            del vs, bs
+            futs.append(pool.submit(oracle.rollout_argmin, prob, vh, bh, index_base=lo,
+                                    incumbent=INC_MAX, integ="rect", want_costs=True))
+        refs = [f.result() for f in futs]
+    out = torch.empty(RESULT_BYTES, dtype=torch.uint8, device="cuda")
+    engine.select_winner(gathered, incumbent=INC_MAX, out=out)
+    got = engine.fetch(out)
+    best = min(range(world), key=lambda r: (refs[r][0].cost, refs[r][0].index))
+    ref = refs[best][0]
+    if got.index != ref.index:           # only a near-tie below the ulp noise
+        lo_g = shard_range(n, 0, world)[1]
+        costs = {r: refs[r][1] for r in range(world)}
+        r_got = next(r for r in range(world) if shard_range(n, r, world)[0] <= got.index
+                     < shard_range(n, r, world)[1])
+        c_got = costs[r_got][got.index - shard_range(n, r_got, world)[0]]
+        gap = abs(c_got - ref.cost) / abs(ref.cost)
+        assert gap < 1e-13, (got.index, ref.index, gap, lo_g)
+    else:
+        assert (got.v, got.beta, got.found) == (ref.v, ref.beta, 1)
+        _close_traj(got, ref, ns)
+        assert math.isclose(got.cost, ref.cost, rel_tol=COST_RTOL)
+
+
+def test_exchange_chain_two_ranks_on_one_gpu(engine, tmp_path):
+    """The multi-GPU chained exchange (mpc_episode_exchange_step: one launch
+    per rank and step + one all_gather of the 536-B candidates; flush by
+    mpc_episode_exchange_flush) rehearsed with 2 gloo ranks sharing this GPU
+    (two child processes): both ranks log exactly the steps of one rank
+    running the single-GPU chained episode over all the candidates, restarts
+    and the final global winner included."""
+    import json
+    import os
+    import socket
+    import subprocess
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.episode import DeviceEpisode
+    n_total, ns, steps, world = 60_000, 10, 70, 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    procs = [subprocess.Popen([sys.executable, os.path.join(repo, "tests", "dist_rank.py"),
+                               str(r), str(world), str(port), str(n_total), str(ns), str(steps),
+                               str(tmp_path / f"rank{r}.json")], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+             for r in range(world)]
+    outs = [p.communicate(timeout=240)[0] for p in procs]
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o.decode()[-3000:]
+    ranks = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
+    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
+    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
+    pool = [engine.sample_controls(V, B, n_total, ns, 4100 + i) for i in range(4)]
+    one = DeviceEpisode(engine, n_total, ns, integrator="rect+cum", chain=True, log_capacity=256,
+                        max_steps=40)
+    for i in range(steps):
+        one.step(controls=pool[i % 4])
+    one.flush()
+    want = [[r.step, r.index, r.cost, r.x, r.y, r.phi, r.v, r.beta, r.p, r.episode, r.status]
+            for r in one.read_log()]
+    assert len(want) == steps and len({w[9] for w in want}) >= 2      # a restart inside
+    for rk in ranks:
+        assert rk["chain_error"] == 0
+        assert rk["log"] == want
+    assert ranks[0]["winner"] == ranks[1]["winner"] == one.local.cpu().tolist()
+
+
 def test_ties_resolve_to_lowest_index(engine):
     from diplomjourney_amd.abi import make_problem
     prob = make_problem(0, 0, 0, 2, 3, 0, 0, 0.5, 0.05, 0.1)
