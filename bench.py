@@ -497,8 +497,7 @@ def stream_ceiling(ep, pool, reps=100, warm=100):
     import torch
     lib = ep.lib
     n, ns = ep.n_local, ep.n_steps
-    grid = min(-(-n // 512), 2048)
-    sink = torch.empty(grid * 256, dtype=torch.int64, device=pool[0][0].device)
+    sink = torch.empty(2048 * 256, dtype=torch.int64, device=pool[0][0].device)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     def one(i):
@@ -567,7 +566,9 @@ INPUTS_DOC = {
     "resident": "per step a distinct synthetic candidate batch already in HBM (generated "
                 "before the timed region by the device sampler: reference grid around "
                 "v=0.5, beta=0, const-control prefix); the step = rollout/arg-min + "
-                "finalize/episode update",
+                "finalize/episode update.  It does NOT regenerate the grid around the "
+                "step's chosen control as the reference does (math_model_tree.py:543-545): "
+                "that is the sampled / generated modes (other_inputs / generated_inputs)",
     "sampled": "per step the device sampler regenerates the candidates on the grid around "
                "the episode's current control (the reference's per-step grid); the step = "
                "sampler + rollout/arg-min + finalize/episode update",

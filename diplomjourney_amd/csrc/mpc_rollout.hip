@@ -77,6 +77,36 @@ int64_t rollout_grid(int64_t n_cand) {
   return std::max<int64_t>(1, std::min<int64_t>(cdiv(n_cand, kBlock * CPL), kMaxBlocks));
 }
 
+// The aligned path's grid (streaming, chained and probe kernels: 5 waves per
+// SIMD, 5 blocks per CU): ONE resident round of blocks, each striding over the
+// same number of 512-candidate tiles — at most the blocks resident at once
+// minus one (a chained launch's block 0 holds a slot), reduced until the tiles
+// divide evenly.  One block per tile would leave a second, partial round of
+// tiles dispatched as the first round ends (at config C 1954 tiles over 1279
+// slots: 675 of them) whose tail streams at half occupancy; the balanced grid
+// (977 blocks x 2 tiles there) ends all blocks together.
+int64_t wide_grid(int64_t n_cand) {
+  static int64_t cap[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+  if (cap[dev] == 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu,
+            reinterpret_cast<const void*>(&k_rollout_argmin_stream<MPC_INTEG_RECT, kRotCum, true>),
+            kBlock, 0) != hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus < 1)
+      cus = 256;
+    cap[dev] = std::max<int64_t>(1, std::min<int64_t>(static_cast<int64_t>(per_cu) * cus - 1,
+                                                      kMaxBlocks));
+  }
+  const int64_t n_tiles = std::max<int64_t>(1, cdiv(n_cand, kBlock * kCplWide));
+  return cdiv(n_tiles, cdiv(n_tiles, cap[dev]));
+}
+
 template <int V>
 using IC = std::integral_constant<int, V>;
 template <bool V>
@@ -153,7 +183,7 @@ int64_t fused_grid(int64_t n_cand) {
 int64_t partial_count(const double* v_sc, const double* beta_sc, int64_t n_cand,
                       bool with_states) {
   const bool wide = !with_states && wide_ok(v_sc, beta_sc, n_cand);
-  return wide ? rollout_grid<kCplWide>(n_cand) : rollout_grid<1>(n_cand);
+  return wide ? wide_grid(n_cand) : rollout_grid<1>(n_cand);
 }
 
 // The streaming kernel: wide (CPL = kCplWide) or scalar path.
@@ -165,7 +195,7 @@ void launch_rollout(hipStream_t st, int32_t integrator, const Consts& K, const C
     constexpr int I = decltype(integ)::value;
     constexpr int R = decltype(rot)::value;
     if (wide)
-      k_rollout_argmin_stream<I, R, KDEV><<<rollout_grid<kCplWide>(n_cand), kBlock, 0, st>>>(
+      k_rollout_argmin_stream<I, R, KDEV><<<wide_grid(n_cand), kBlock, 0, st>>>(
           K, Kdev, v, b, n_cand, n_steps, part);
     else
       k_rollout_argmin<1, I, R, false, KDEV>
@@ -334,8 +364,9 @@ int mpc_stream_probe(const double* v_sc, const double* beta_sc, int64_t n_cand,
   if (!v_sc || !beta_sc || n_cand < 2 || n_steps < 1 || n_steps > MPC_MAX_STEPS || !sink)
     return MPC_ERR_ARG;
   if (!wide_ok(v_sc, beta_sc, n_cand)) return MPC_ERR_UNSUPPORTED;
-  const int64_t grid = rollout_grid<kCplWide>(n_cand);
-  if (sink_bytes < static_cast<size_t>(grid) * kBlock * sizeof(uint64_t)) return MPC_ERR_WORKSPACE;
+  const int64_t grid = wide_grid(n_cand);
+  if (sink_bytes < static_cast<size_t>(kMaxBlocks) * kBlock * sizeof(uint64_t))
+    return MPC_ERR_WORKSPACE;
   k_stream_probe<<<grid, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
       v_sc, beta_sc, n_cand, n_steps, static_cast<uint64_t*>(sink));
   return last_hip_status();
@@ -554,13 +585,15 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
   EpisodeState* S = static_cast<EpisodeState*>(state);
   int e;
   const int pl2 = frexp(cfg->L, &e) == 0.5 ? 1 : 0;   // as consts_from_problem decides
-  const int64_t grid = rollout_grid<kCplWide>(n_cand) + 1;
-  const int n_part_prev = static_cast<int>(rollout_grid<kCplWide>(n_cand));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   constexpr int I = MPC_INTEG_RECT;
+  // block 0 + the aligned path's tile blocks; the previous step's records are
+  // as many (same n_cand), and as many as mpc_episode_finalize reduces
+  const int64_t tiles = wide_grid(n_cand);
+  const int n_part_prev = static_cast<int>(tiles);
   auto launch = [&](auto pl2_tag) {
     constexpr bool P = decltype(pl2_tag)::value;
-    k_episode_chain<I, kRotCum, kChainFin, P><<<grid, kBlock, 0, st>>>(
+    k_episode_chain<I, kRotCum, kChainFin, P><<<tiles + 1, kBlock, 0, st>>>(
         S, epoch, v_sc, beta_sc, n_cand, n_steps, static_cast<Rec*>(ws), has_prev,
         static_cast<const Rec*>(ws_prev), n_part_prev, v_prev, beta_prev, index_base, out_prev,
         nullptr, 0, *cfg, log, log_capacity);
@@ -590,7 +623,7 @@ int mpc_episode_exchange_step(const mpc_episode_config_t* cfg, void* state, uint
   EpisodeState* S = static_cast<EpisodeState*>(state);
   int e;
   const int pl2 = frexp(cfg->L, &e) == 0.5 ? 1 : 0;
-  const int64_t grid = rollout_grid<kCplWide>(n_cand) + 1;
+  const int64_t grid = wide_grid(n_cand) + 1;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   constexpr int I = MPC_INTEG_RECT;
   auto launch = [&](auto pl2_tag) {

@@ -155,8 +155,8 @@ int mpc_select_winner(const mpc_result_t* results, int32_t n, double incumbent,
  * control ring, no rollout arithmetic — so its duration is the read-only
  * HBM ceiling of the rollout's own access pattern at this size (bench.py's
  * roofline `stream_ceiling`).  Aligned path only (n_cand even, 16-B aligned
- * controls); sink: device scratch of >= grid * 256 * 8 bytes, where grid =
- * min(ceil(n_cand / 512), 2048) (almost never written). */
+ * controls); sink: device scratch of >= 2048 * 256 * 8 bytes (almost never
+ * written). */
 int mpc_stream_probe(const double* v_sc, const double* beta_sc, int64_t n_cand,
                      int32_t n_steps, void* sink, size_t sink_bytes, mpc_stream_t stream);
 
