@@ -15,6 +15,7 @@
 #include <type_traits>
 
 #include "../../include/mpc_rollout.h"
+#include "mpc_comm.h"
 #include "mpc_episode.h"
 #include "mpc_fulltree.h"
 #include "mpc_kernels.h"
@@ -75,36 +76,6 @@ bool wide_ok(const double* v_sc, const double* beta_sc, int64_t n) {
 template <int CPL>
 int64_t rollout_grid(int64_t n_cand) {
   return std::max<int64_t>(1, std::min<int64_t>(cdiv(n_cand, kBlock * CPL), kMaxBlocks));
-}
-
-// The aligned path's grid (streaming, chained and probe kernels: 5 waves per
-// SIMD, 5 blocks per CU): ONE resident round of blocks, each striding over the
-// same number of 512-candidate tiles — at most the blocks resident at once
-// minus one (a chained launch's block 0 holds a slot), reduced until the tiles
-// divide evenly.  One block per tile would leave a second, partial round of
-// tiles dispatched as the first round ends (at config C 1954 tiles over 1279
-// slots: 675 of them) whose tail streams at half occupancy; the balanced grid
-// (977 blocks x 2 tiles there) ends all blocks together.
-int64_t wide_grid(int64_t n_cand) {
-  static int64_t cap[16] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
-  if (cap[dev] == 0) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu,
-            reinterpret_cast<const void*>(&k_rollout_argmin_stream<MPC_INTEG_RECT, kRotCum, true>),
-            kBlock, 0) != hipSuccess ||
-        per_cu < 1)
-      per_cu = 1;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus < 1)
-      cus = 256;
-    cap[dev] = std::max<int64_t>(1, std::min<int64_t>(static_cast<int64_t>(per_cu) * cus - 1,
-                                                      kMaxBlocks));
-  }
-  const int64_t n_tiles = std::max<int64_t>(1, cdiv(n_cand, kBlock * kCplWide));
-  return cdiv(n_tiles, cdiv(n_tiles, cap[dev]));
 }
 
 template <int V>
@@ -183,7 +154,7 @@ int64_t fused_grid(int64_t n_cand) {
 int64_t partial_count(const double* v_sc, const double* beta_sc, int64_t n_cand,
                       bool with_states) {
   const bool wide = !with_states && wide_ok(v_sc, beta_sc, n_cand);
-  return wide ? wide_grid(n_cand) : rollout_grid<1>(n_cand);
+  return wide ? rollout_grid<kCplWide>(n_cand) : rollout_grid<1>(n_cand);
 }
 
 // The streaming kernel: wide (CPL = kCplWide) or scalar path.
@@ -195,7 +166,7 @@ void launch_rollout(hipStream_t st, int32_t integrator, const Consts& K, const C
     constexpr int I = decltype(integ)::value;
     constexpr int R = decltype(rot)::value;
     if (wide)
-      k_rollout_argmin_stream<I, R, KDEV><<<wide_grid(n_cand), kBlock, 0, st>>>(
+      k_rollout_argmin_stream<I, R, KDEV><<<rollout_grid<kCplWide>(n_cand), kBlock, 0, st>>>(
           K, Kdev, v, b, n_cand, n_steps, part);
     else
       k_rollout_argmin<1, I, R, false, KDEV>
@@ -364,7 +335,7 @@ int mpc_stream_probe(const double* v_sc, const double* beta_sc, int64_t n_cand,
   if (!v_sc || !beta_sc || n_cand < 2 || n_steps < 1 || n_steps > MPC_MAX_STEPS || !sink)
     return MPC_ERR_ARG;
   if (!wide_ok(v_sc, beta_sc, n_cand)) return MPC_ERR_UNSUPPORTED;
-  const int64_t grid = wide_grid(n_cand);
+  const int64_t grid = rollout_grid<kCplWide>(n_cand);
   if (sink_bytes < static_cast<size_t>(kMaxBlocks) * kBlock * sizeof(uint64_t))
     return MPC_ERR_WORKSPACE;
   k_stream_probe<<<grid, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
@@ -587,9 +558,9 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
   const int pl2 = frexp(cfg->L, &e) == 0.5 ? 1 : 0;   // as consts_from_problem decides
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   constexpr int I = MPC_INTEG_RECT;
-  // block 0 + the aligned path's tile blocks; the previous step's records are
-  // as many (same n_cand), and as many as mpc_episode_finalize reduces
-  const int64_t tiles = wide_grid(n_cand);
+  // block 0 + one block per tile; the previous step's records are as many
+  // (same n_cand), and as many as mpc_episode_finalize reduces
+  const int64_t tiles = rollout_grid<kCplWide>(n_cand);
   const int n_part_prev = static_cast<int>(tiles);
   auto launch = [&](auto pl2_tag) {
     constexpr bool P = decltype(pl2_tag)::value;
@@ -623,7 +594,7 @@ int mpc_episode_exchange_step(const mpc_episode_config_t* cfg, void* state, uint
   EpisodeState* S = static_cast<EpisodeState*>(state);
   int e;
   const int pl2 = frexp(cfg->L, &e) == 0.5 ? 1 : 0;
-  const int64_t grid = wide_grid(n_cand) + 1;
+  const int64_t grid = rollout_grid<kCplWide>(n_cand) + 1;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   constexpr int I = MPC_INTEG_RECT;
   auto launch = [&](auto pl2_tag) {
@@ -652,6 +623,74 @@ int mpc_episode_exchange_flush(const mpc_episode_config_t* cfg, void* state, int
       <<<1, kFinBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
           *cfg, static_cast<EpisodeState*>(state), gathered, n_gathered, out, log, log_capacity);
   return last_hip_status();
+}
+
+// ----------------------------- RCCL exchange --------------------------------
+int mpc_comm_unique_id(void* id) {
+  const rccl::Api& r = rccl::api();
+  if (!id) return MPC_ERR_ARG;
+  if (!r.ok) return MPC_ERR_UNSUPPORTED;
+  rccl::UniqueId u;
+  if (r.get_unique_id(&u) != rccl::kSuccess) return MPC_ERR_HIP;
+  memcpy(id, &u, sizeof(u));
+  return MPC_OK;
+}
+
+int mpc_comm_init_rank(const void* id, int32_t n_ranks, int32_t rank, mpc_comm_t* comm) {
+  const rccl::Api& r = rccl::api();
+  if (!id || !comm || n_ranks < 1 || rank < 0 || rank >= n_ranks) return MPC_ERR_ARG;
+  if (!r.ok) return MPC_ERR_UNSUPPORTED;
+  rccl::UniqueId u;
+  memcpy(&u, id, sizeof(u));
+  rccl::Comm c = nullptr;
+  if (r.comm_init_rank(&c, n_ranks, u, rank) != rccl::kSuccess) return MPC_ERR_HIP;
+  *comm = reinterpret_cast<mpc_comm_t>(c);
+  return MPC_OK;
+}
+
+int mpc_comm_init_all(int32_t n_devices, const int32_t* devices, mpc_comm_t* comms) {
+  const rccl::Api& r = rccl::api();
+  if (n_devices < 1 || !comms) return MPC_ERR_ARG;
+  if (!r.ok) return MPC_ERR_UNSUPPORTED;
+  rccl::Comm* c = reinterpret_cast<rccl::Comm*>(comms);
+  return r.comm_init_all(c, n_devices, devices) == rccl::kSuccess ? MPC_OK : MPC_ERR_HIP;
+}
+
+int mpc_comm_destroy(mpc_comm_t comm) {
+  const rccl::Api& r = rccl::api();
+  if (!comm) return MPC_ERR_ARG;
+  if (!r.ok) return MPC_ERR_UNSUPPORTED;
+  return r.comm_destroy(reinterpret_cast<rccl::Comm>(comm)) == rccl::kSuccess ? MPC_OK
+                                                                              : MPC_ERR_HIP;
+}
+
+int mpc_exchange_allgather(mpc_comm_t comm, const mpc_candidate_t* local,
+                           mpc_candidate_t* gathered, mpc_stream_t stream) {
+  const rccl::Api& r = rccl::api();
+  if (!comm || !local || !gathered) return MPC_ERR_ARG;
+  if (!r.ok) return MPC_ERR_UNSUPPORTED;
+  return r.all_gather(local, gathered, sizeof(mpc_candidate_t), rccl::kUint8,
+                      reinterpret_cast<rccl::Comm>(comm),
+                      reinterpret_cast<hipStream_t>(stream)) == rccl::kSuccess
+             ? MPC_OK
+             : MPC_ERR_HIP;
+}
+
+int mpc_exchange_allgather_group(int32_t n, const mpc_comm_t* comms,
+                                 const mpc_candidate_t* const* local,
+                                 mpc_candidate_t* const* gathered, const mpc_stream_t* streams) {
+  const rccl::Api& r = rccl::api();
+  if (n < 1 || !comms || !local || !gathered || !streams) return MPC_ERR_ARG;
+  if (!r.ok) return MPC_ERR_UNSUPPORTED;
+  if (r.group_start() != rccl::kSuccess) return MPC_ERR_HIP;
+  int st = MPC_OK;
+  for (int i = 0; i < n; ++i)
+    if (r.all_gather(local[i], gathered[i], sizeof(mpc_candidate_t), rccl::kUint8,
+                     reinterpret_cast<rccl::Comm>(comms[i]),
+                     reinterpret_cast<hipStream_t>(streams[i])) != rccl::kSuccess)
+      st = MPC_ERR_HIP;
+  if (r.group_end() != rccl::kSuccess) st = MPC_ERR_HIP;
+  return st;
 }
 
 int mpc_episode_chain_error(const void* state, int32_t* error, mpc_stream_t stream) {

@@ -33,13 +33,15 @@ EXPORTS = (
     "mpc_episode_expand", "mpc_episode_advance", "mpc_episode_sample", "mpc_episode_partials",
     "mpc_episode_finalize", "mpc_episode_rollout", "mpc_episode_step", "mpc_episode_chain_step",
     "mpc_episode_chain_error", "mpc_episode_exchange_step", "mpc_episode_exchange_flush",
+    "mpc_comm_unique_id", "mpc_comm_init_rank", "mpc_comm_init_all", "mpc_comm_destroy",
+    "mpc_exchange_allgather", "mpc_exchange_allgather_group",
     "mpc_episode_generate_workspace_bytes", "mpc_episode_generate_step",
     "mpc_fulltree_workspace_bytes", "mpc_fulltree_argmin",
     "mpc_fulltree_batched_workspace_bytes", "mpc_fulltree_argmin_batched",
 )
 
 HIPCC_FLAGS = [
-    "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+    "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ldl",
     # One IEEE rounding per reference operator: no a*b+c contraction.
     "-ffp-contract=off",
     "-Wall",
@@ -54,6 +56,24 @@ def build(verbose=False):
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     return LIB_PATH
+
+
+C_HOST_SRC = os.path.join(REPO_DIR, "tests", "c_host", "exchange_episode.cpp")
+C_HOST_BIN = os.path.join(REPO_DIR, "tests", "_build", "exchange_episode")
+
+
+def build_c_host(verbose=False):
+    """The test-side C++ host program (tests/c_host): the sharded episode
+    through the C ABI and RCCL only, linked against the in-tree library."""
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    os.makedirs(os.path.dirname(C_HOST_BIN), exist_ok=True)
+    cmd = [hipcc, "--offload-arch=gfx950", "-O2", "-std=c++17", "-I",
+           os.path.join(REPO_DIR, "include"), "-o", C_HOST_BIN, C_HOST_SRC, "-L", PKG_DIR,
+           "-lmpc_rollout", "-Wl,-rpath,$ORIGIN/../../diplomjourney_amd"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return C_HOST_BIN
 
 
 def needs_build():

@@ -323,6 +323,26 @@ int mpc_episode_exchange_flush(const mpc_episode_config_t* cfg, void* state, int
                                const mpc_candidate_t* gathered, int32_t n_gathered,
                                mpc_result_t* out, mpc_episode_log_t* log, int32_t log_capacity,
                                mpc_stream_t stream);
+/* The exchange's collective for a non-Python host: an RCCL
+ * communicator per GPU — one process driving all local GPUs (a clique,
+ * mpc_comm_init_all) or one rank per process (mpc_comm_unique_id on rank 0,
+ * shared by the caller, then mpc_comm_init_rank on every rank) — and the
+ * per-step all_gather of the ranks' mpc_candidate_t (device pointers; the
+ * gathered array has one record per rank, in rank order).  RCCL is loaded at
+ * run time (librccl.so.1); MPC_ERR_UNSUPPORTED if it cannot be.
+ * mpc_exchange_allgather_group issues n communicators' all_gathers inside one
+ * RCCL group (the single-process clique: one thread, one stream per GPU). */
+typedef struct mpc_comm* mpc_comm_t;
+int mpc_comm_unique_id(void* id /* 128 bytes */);
+int mpc_comm_init_rank(const void* id, int32_t n_ranks, int32_t rank, mpc_comm_t* comm);
+int mpc_comm_init_all(int32_t n_devices, const int32_t* devices, mpc_comm_t* comms);
+int mpc_comm_destroy(mpc_comm_t comm);
+int mpc_exchange_allgather(mpc_comm_t comm, const mpc_candidate_t* local,
+                           mpc_candidate_t* gathered, mpc_stream_t stream);
+int mpc_exchange_allgather_group(int32_t n, const mpc_comm_t* comms,
+                                 const mpc_candidate_t* const* local,
+                                 mpc_candidate_t* const* gathered, const mpc_stream_t* streams);
+
 /* Generated controls (one GPU): one MPC step of the device-resident episode
  * whose candidates are never materialised — the same candidates, bit for bit,
  * as mpc_episode_sample followed by mpc_episode_step (advance = cfg) on the

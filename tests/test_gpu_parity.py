@@ -315,6 +315,47 @@ def test_exchange_chain_two_ranks_on_one_gpu(engine, tmp_path):
     assert ranks[0]["winner"] == ranks[1]["winner"] == one.local.cpu().tolist()
 
 
+def test_c_host_exchange_episode(engine, tmp_path):
+    """A C++ host with no Python (tests/c_host/exchange_episode.cpp): one
+    process, an RCCL clique of the visible GPUs (here 1) from
+    mpc_comm_init_all, per MPC step mpc_episode_exchange_step on every GPU and
+    one grouped all_gather (mpc_exchange_allgather_group); flushed by
+    mpc_episode_exchange_flush.  Its episode log and final winner equal, byte
+    for byte, the single-GPU chained episode driven from Python."""
+    import ctypes
+    import os
+    import struct
+    import subprocess
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd import native
+    from diplomjourney_amd.abi import LOG_BYTES, RESULT_BYTES
+    from diplomjourney_amd.episode import DeviceEpisode, reference_episode_config
+    n_total, ns, steps, seed0 = 40_000, 10, 60, 4200
+    cfg = reference_episode_config(max_steps=40)
+    V, B = mmt.vector_of_velocities(0.5), mmt.vector_of_beta_angles(0.0)
+    blob = (struct.pack("<6i", 1, ns, steps, len(V), len(B), 0) + struct.pack("<qQ", n_total, seed0)
+            + bytes(cfg) + struct.pack(f"<{len(V)}d", *V) + struct.pack(f"<{len(B)}d", *B))
+    (tmp_path / "in.bin").write_bytes(blob)
+    assert os.path.exists(native.C_HOST_BIN), "built by __graft_entry__.build()"
+    r = subprocess.run([native.C_HOST_BIN, str(tmp_path / "in.bin"), str(tmp_path / "out.bin")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = (tmp_path / "out.bin").read_bytes()
+    Vd = torch.tensor(V, dtype=torch.float64, device="cuda")
+    Bd = torch.tensor(B, dtype=torch.float64, device="cuda")
+    pool = [engine.sample_controls(Vd, Bd, n_total, ns, seed0 + k) for k in range(4)]
+    one = DeviceEpisode(engine, n_total, ns, integrator="rect+cum", chain=True, log_capacity=256,
+                        max_steps=40)
+    for i in range(steps):
+        one.step(controls=pool[i % 4])
+    one.flush()
+    want = b"".join(bytes(rec) for rec in one.read_log())
+    assert len(want) == steps * LOG_BYTES
+    assert len({rec.episode for rec in one.read_log()}) >= 2         # a restart inside
+    assert out[:steps * LOG_BYTES] == want
+    assert out[steps * LOG_BYTES:steps * LOG_BYTES + RESULT_BYTES] == bytes(one.local.cpu().numpy())
+
+
 def test_ties_resolve_to_lowest_index(engine):
     from diplomjourney_amd.abi import make_problem
     prob = make_problem(0, 0, 0, 2, 3, 0, 0, 0.5, 0.05, 0.1)

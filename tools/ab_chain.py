@@ -1,55 +1,69 @@
-"""A/B of the chained step's launch knobs (MPC_CHAIN_BLOCKS, MPC_ANYORDER) at
-config C: per variant, 300 warm + 200 timed chained launches (HIP events,
-rotating over 8 resident batches), variants interleaved for R rounds.
-Timing only (a variant's flush is not used).
-    python tools/ab_chain.py [rounds] VAR=VAL,VAR=VAL ...   ("-" = defaults)"""
+"""Same-box A/B of library builds at config C: for each library (env
+DIPLOMJOURNEY_MPC_LIB=<path>, one child process per measurement, interleaved
+for R rounds) the chained launch and the plain streaming kernel, 300 warm +
+200 timed back-to-back launches between HIP events over 8 resident batches.
+    python tools/ab_chain.py ROUNDS LIB [LIB ...]      (LIB "-" = in-tree build)"""
+import json
 import os
+import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, REPO)
-
-import torch  # noqa: E402
-
-from diplomjourney_amd import math_model_tree as mmt  # noqa: E402
-from diplomjourney_amd.episode import DeviceEpisode  # noqa: E402
-from diplomjourney_amd.expansion import Expansion  # noqa: E402
 
 
-def main():
-    rounds = int(sys.argv[1])
-    variants = sys.argv[2:]
+def child():
+    sys.path.insert(0, REPO)
+    import torch
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.episode import DeviceEpisode
+    from diplomjourney_amd.expansion import Expansion
     n = int(os.environ.get("AB_N", "1000000"))
     ns = int(os.environ.get("AB_NS", "10"))
     eng = Expansion("cuda:0")
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
     pool = [eng.sample_controls(V, B, n, ns, 0x5EED0000 + i) for i in range(8)]
-    res = {v: [] for v in variants}
+    ep = DeviceEpisode(eng, n, ns, integrator="rect+cum", chain=True, log_capacity=8192)
+    out = {}
+    for name, fn in (("chain", lambda i: ep.step(controls=pool[i % 8])),
+                     ("stream", lambda i: (setattr(ep, "cur", pool[i % 8]), ep.partials()))):
+        for i in range(300):
+            fn(i)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(200):
+            fn(i + 3)
+        e1.record()
+        torch.cuda.synchronize()
+        out[name] = e0.elapsed_time(e1) / 200 * 1e3
+        ep.flush()
+    print("AB " + json.dumps(out), flush=True)
+
+
+def main():
+    if sys.argv[1] == "--child":
+        return child()
+    rounds, libs = int(sys.argv[1]), sys.argv[2:]
+    res = {lib: [] for lib in libs}
     for _ in range(rounds):
-        for var in variants:
-            for k in ("MPC_CHAIN_BLOCKS", "MPC_ANYORDER"):
-                os.environ.pop(k, None)
-            if var != "-":
-                for kv in var.split(","):
-                    k, val = kv.split("=")
-                    os.environ[k] = val
-            ep = DeviceEpisode(eng, n, ns, integrator="rect+cum", chain=True, log_capacity=8192)
-            for i in range(300):
-                ep.step(controls=pool[i % 8])
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for i in range(200):
-                ep.step(controls=pool[(i + 3) % 8])
-            e1.record()
-            torch.cuda.synchronize()
-            res[var].append(e0.elapsed_time(e1) / 200 * 1e3)
-            ep._pending = None
-            del ep
-    for var, xs in res.items():
-        print(f"{var:40s} " + " ".join(f"{x:6.2f}" for x in xs) + f"   min {min(xs):6.2f} us",
+        for lib in libs:
+            env = dict(os.environ)
+            if lib != "-":
+                env["DIPLOMJOURNEY_MPC_LIB"] = os.path.abspath(lib)
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child"], env=env,
+                               capture_output=True, text=True, timeout=300)
+            line = [ln for ln in r.stdout.splitlines() if ln.startswith("AB ")]
+            if r.returncode != 0 or not line:
+                print(lib, "failed", r.stderr[-800:], flush=True)
+                return 1
+            res[lib].append(json.loads(line[0][3:]))
+    for lib, xs in res.items():
+        ch = [x["chain"] for x in xs]
+        stv = [x["stream"] for x in xs]
+        print(f"{lib:32s} chain " + " ".join(f"{x:6.2f}" for x in ch) + f"  min {min(ch):6.2f}"
+              f" | stream " + " ".join(f"{x:6.2f}" for x in stv) + f"  min {min(stv):6.2f} us",
               flush=True)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
