@@ -527,7 +527,7 @@ __device__ void advance_from_candidates(const mpc_episode_config_t& c, EpisodeSt
                                         const mpc_candidate_t* __restrict__ g, int n,
                                         mpc_result_t* __restrict__ out,
                                         mpc_episode_log_t* __restrict__ log, int cap,
-                                        bool end_chain) {
+                                        uint32_t publish_epoch) {
   __shared__ uint64_t s_head[kStagedWords];
   __shared__ mpc_episode_log_t s_log;
   __shared__ mpc_episode_log_t* s_slot;
@@ -566,15 +566,17 @@ __device__ void advance_from_candidates(const mpc_episode_config_t& c, EpisodeSt
     __builtin_memcpy(s_head, &H, sizeof(EpisodeHead));
   }
   __syncthreads();
-  store_update(&S->h, s_head, s_slot, reinterpret_cast<const uint64_t*>(&s_log),
-               end_chain ? S->chain_pub : nullptr, kPubWords);
+  // publish_epoch 0: the update ends the chain (tags cleared); else it
+  // publishes the next step's constants (a chained exchange step's block 0)
+  store_update(&S->h, s_head, s_slot, reinterpret_cast<const uint64_t*>(&s_log), S->chain_pub,
+               kPubWords, publish_epoch);
 }
 
 template <int INTEG, int ROT>
 __global__ __launch_bounds__(kFinBlock) void k_episode_advance_cand(
     mpc_episode_config_t c, EpisodeState* __restrict__ S, const mpc_candidate_t* __restrict__ g,
     int n, mpc_result_t* __restrict__ out, mpc_episode_log_t* __restrict__ log, int cap) {
-  advance_from_candidates<INTEG, ROT>(c, S, g, n, out, log, cap, true);
+  advance_from_candidates<INTEG, ROT>(c, S, g, n, out, log, cap, 0u);
 }
 
 // A tile block's record in an exchange step: ONE 16-B `sc1` store {cost key,
@@ -779,18 +781,22 @@ __global__ __launch_bounds__(kBlock, kChainWaves) void k_episode_chain(
   static_assert(ROT == kRotCum, "chained steps need the pose-independent recurrence");
   if (blockIdx.x == 0) {
     if (has_prev) {
+      // the completion of step k-1 publishes step k's constants itself, from
+      // its LDS copy of the updated head (store_update)
       if constexpr (MODE == kChainFin) {
         const Consts Kp = S->h.K;
-        const EpisodeHook hook{&S->h, log, cap, nullptr, 0};
+        const EpisodeHook hook{&S->h, log, cap, S->chain_pub, kPubWords, epoch};
         finalize_block<INTEG, ROT, true, kBlock, false>(part_prev, n_part_prev, Kp, v_prev,
                                                         b_prev, n_cand, n_steps, index_base,
                                                         S->h.incumbent, out_prev, ecfg, hook);
       } else {
         advance_from_candidates<INTEG, ROT>(ecfg, S, gathered, n_gathered, out_prev, log, cap,
-                                            false);
+                                            epoch);
       }
+      __syncthreads();   // (the wheelbase check below reads the stored head)
+    } else {
+      chain_publish(S, epoch);   // no previous step: the head as reset / last updated
     }
-    chain_publish(S, epoch);
     // The host picked PL2 from the caller's cfg; the tile blocks use the
     // published head's wheelbase terms.  If those disagree (a cfg other than
     // the one the state was reset with) every dphi would be formed with the
@@ -869,7 +875,7 @@ __global__ __launch_bounds__(kBlock, kChainWaves) void k_episode_chain(
         }
         uint32_t it = 0;
         while (!fin && !(fin = chain_read(S, epoch, s_w, s_tag)) && ++it < kChainSpinLimit)
-          __builtin_amdgcn_s_sleep(32);
+          __builtin_amdgcn_s_sleep(4);
         if (!fin && threadIdx.x == 0) S->chain_error = 1u;
       }
       __syncthreads();

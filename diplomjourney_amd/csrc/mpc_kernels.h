@@ -688,8 +688,9 @@ struct EpisodeHook {  // single-GPU episode: finalize also advances it
   EpisodeHead* H;     // nullptr: no hook
   mpc_episode_log_t* log;
   int cap;
-  uint64_t* chain_pub = nullptr;   // cleared with the update (ends a chain of chained steps)
+  uint64_t* chain_pub = nullptr;   // cleared with the update (ends a chain of chained steps) ...
   int chain_pub_words = 0;
+  uint32_t publish_epoch = 0;      // ... or, nonzero, the next step's constants published
 };
 constexpr int kHeadWords = static_cast<int>(sizeof(EpisodeHead) / 8);
 constexpr int kStaleWords = static_cast<int>(sizeof(StaleTraj) / 8);
@@ -707,13 +708,30 @@ __device__ __forceinline__ mpc_episode_log_t* log_slot(mpc_episode_log_t* log, i
 // The episode update's stores, one 8-B word per lane (called by every thread
 // after a barrier; thread 0 staged the head and the log record in LDS): a
 // single lane's ~40 stores serialise in the address path for ~0.7 us.
+// epoch != 0 (a chained launch's block 0): instead of clearing the chain
+// tags, publish the updated head's Consts and t as epoch-tagged words (the
+// layout of EpisodeState::chain_pub: Consts' dwords, then t's two) straight
+// from the LDS copy — not re-read from HBM after the head's stores, which
+// would put a store drain and a load round trip in front of the publication.
 __device__ __forceinline__ void store_update(EpisodeHead* H, const uint64_t* s_head,
                                              mpc_episode_log_t* slot, const uint64_t* s_log,
-                                             uint64_t* chain_pub, int chain_words) {
+                                             uint64_t* chain_pub, int chain_words,
+                                             uint32_t epoch = 0) {
   const int q = threadIdx.x;
+  if (chain_pub && q < chain_words) {
+    if (epoch) {
+      constexpr int kKWords = static_cast<int>(sizeof(Consts) / 4);
+      const uint32_t* dw = reinterpret_cast<const uint32_t*>(s_head);
+      const uint32_t d =
+          q < kKWords ? dw[q] : dw[offsetof(EpisodeHead, t) / 4 + (q - kKWords)];
+      __hip_atomic_store(&chain_pub[q], (static_cast<uint64_t>(d) << 32) | epoch,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      chain_pub[q] = 0ull;
+    }
+  }
   if (q < kStagedWords) reinterpret_cast<uint64_t*>(H)[q] = s_head[q];   // head, then StaleTraj
   if (slot && q < kLogWords) reinterpret_cast<uint64_t*>(slot)[q] = s_log[q];
-  if (chain_pub && q < chain_words) chain_pub[q] = 0ull;
 }
 
 __device__ void episode_hook(const mpc_episode_config_t& c, const EpisodeHook& h,
@@ -863,7 +881,7 @@ __device__ __forceinline__ void finalize_block(
     __syncthreads();
     // the head and the log record back to HBM, the chain tags cleared
     store_update(hook.H, s_head, s_slot, reinterpret_cast<const uint64_t*>(&s_log),
-                 hook.chain_pub, hook.chain_pub_words);
+                 hook.chain_pub, hook.chain_pub_words, hook.publish_epoch);
   }
 }
 
