@@ -177,44 +177,48 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 }
 
 // Both control rows of one step into LDS (v at dst_v, beta at dst_b).  The
-// statement writes only M0 (saved and restored) and `keep`: no SCC-setting
-// instruction (s_add etc.), since hipcc may hold a live SCC across it.
+// addresses are SGPR base + 32-bit VGPR offset (the `saddr` form): the row
+// bases gv / gb (step s's rows: wave-uniform) advance per step on the SALU,
+// the lane's byte offset `voff` is fixed for the tile — no 64-bit per-lane
+// address arithmetic on the VALU in the loop.  The statement writes only M0
+// (saved and restored) and `keep`: no SCC-setting instruction (s_add etc.),
+// since hipcc may hold a live SCC across it.
 // Refilling a slot must not overtake the LDS reads of its previous contents:
 // `read_v`/`read_b` are the registers those reads produced, taken as inputs
 // so hipcc completes the reads (lgkmcnt) before the DMA is issued — without a
 // blanket lgkmcnt(0), which would also wait for unrelated scalar loads.
-__device__ __forceinline__ void glds_pair(const double* gv, const double* gb, uint32_t dst_v,
-                                          uint32_t dst_b) {
+__device__ __forceinline__ void glds_pair(const double* gv, const double* gb, uint32_t voff,
+                                          uint32_t dst_v, uint32_t dst_b) {
   uint32_t keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off" MPC_GLDS_POLICY "\n\t"
       "s_mov_b32 m0, %4\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %2, off" MPC_GLDS_POLICY "\n\t"
+      "global_load_lds_dwordx4 %1, %2" MPC_GLDS_POLICY "\n\t"
+      "s_mov_b32 m0, %5\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %3" MPC_GLDS_POLICY "\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(gv), "v"(gb), "s"(dst_v), "s"(dst_b)
+      : "v"(voff), "s"(gv), "s"(gb), "s"(dst_v), "s"(dst_b)
       : "memory");
 }
 
-__device__ __forceinline__ void glds_refill(const double* gv, const double* gb, uint32_t dst_v,
-                                            uint32_t dst_b, const double2& read_v,
-                                            const double2& read_b) {
+__device__ __forceinline__ void glds_refill(const double* gv, const double* gb, uint32_t voff,
+                                            uint32_t dst_v, uint32_t dst_b,
+                                            const double2& read_v, const double2& read_b) {
   uint32_t keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off" MPC_GLDS_POLICY "\n\t"
       "s_mov_b32 m0, %4\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %2, off" MPC_GLDS_POLICY "\n\t"
+      "global_load_lds_dwordx4 %1, %2" MPC_GLDS_POLICY "\n\t"
+      "s_mov_b32 m0, %5\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %3" MPC_GLDS_POLICY "\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(gv), "v"(gb), "s"(dst_v), "s"(dst_b), "v"(read_v.x), "v"(read_v.y),
+      : "v"(voff), "s"(gv), "s"(gb), "s"(dst_v), "s"(dst_b), "v"(read_v.x), "v"(read_v.y),
         "v"(read_b.x), "v"(read_b.y)
       : "memory");
 }
@@ -269,6 +273,9 @@ __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Const
   const uint32_t ring0 = __builtin_amdgcn_readfirstlane(lds_addr(&g_ring[wv][0][0][0]));
   constexpr uint32_t kSlot = 2 * 64 * sizeof(double2);  // 2 KiB
   auto dst = [&](int slot) { return ring0 + slot * kSlot; };
+  // the lane's byte offset in every control row (< 2^31: the host checks
+  // 8 * ld < 2^31 for the aligned path)
+  const uint32_t voff = static_cast<uint32_t>(c0) * 8u;
   // leading trig coefficients pinned in VGPRs (opaque to the compiler, so not
   // re-materialised per step)
   trig::Leads lead = trig::const_leads();
@@ -285,8 +292,7 @@ __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Const
   for (int pass = 0;; ++pass) {
 #pragma unroll
     for (int u = 0; u < R - 1; ++u)
-      if (u < n_steps)
-        glds_pair(v + u * ld + c0, b + u * ld + c0, dst(u), dst(u) + kSlot / 2);
+      if (u < n_steps) glds_pair(v + u * ld, b + u * ld, voff, dst(u), dst(u) + kSlot / 2);
     if (pass == 0) {
       if constexpr (ROT != kRotCum)
         pre();
@@ -308,7 +314,7 @@ __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Const
         if (st < n_steps) {
           if (st + R - 1 < n_steps) {
             const int sr = st + R - 1, slot = (u + R - 1) % R;   // = the slot read last step
-            glds_refill(v + sr * ld + c0, b + sr * ld + c0, dst(slot), dst(slot) + kSlot / 2, v2,
+            glds_refill(v + sr * ld, b + sr * ld, voff, dst(slot), dst(slot) + kSlot / 2, v2,
                         b2);
             wait_vm<2 * (R - 1)>();   // this step's pair has landed
           } else {
@@ -465,10 +471,10 @@ __global__ __launch_bounds__(kBlock, kStreamWaves) void k_stream_probe(
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     const int64_t c0 = tile * (kBlock * 2) + threadIdx.x * 2;
     if (c0 >= n_cand) continue;   // n_cand even (host check): the pair is valid
+    const uint32_t voff = static_cast<uint32_t>(c0) * 8u;
 #pragma unroll
     for (int u = 0; u < R - 1; ++u)
-      if (u < n_steps) glds_pair(v + u * n_cand + c0, b + u * n_cand + c0, dst(u),
-                                 dst(u) + kSlot / 2);
+      if (u < n_steps) glds_pair(v + u * n_cand, b + u * n_cand, voff, dst(u), dst(u) + kSlot / 2);
     double2 v2 = make_double2(0.0, 0.0), b2 = v2;
 #pragma unroll 1
     for (int s = 0; s < n_steps; s += R) {
@@ -478,8 +484,8 @@ __global__ __launch_bounds__(kBlock, kStreamWaves) void k_stream_probe(
         if (st < n_steps) {
           if (st + R - 1 < n_steps) {
             const int sr = st + R - 1, slot = (u + R - 1) % R;
-            glds_refill(v + sr * n_cand + c0, b + sr * n_cand + c0, dst(slot),
-                        dst(slot) + kSlot / 2, v2, b2);
+            glds_refill(v + sr * n_cand, b + sr * n_cand, voff, dst(slot), dst(slot) + kSlot / 2,
+                        v2, b2);
             wait_vm<2 * (R - 1)>();
           } else {
             wait_vm<0>();

@@ -67,8 +67,11 @@ inline int64_t rollout_blocks(int64_t n_cand) {
 
 int last_hip_status() { return hipGetLastError() == hipSuccess ? MPC_OK : MPC_ERR_HIP; }
 
-bool wide_ok(const double* v_sc, const double* beta_sc, int64_t n) {
-  return (n % kCplWide == 0) && aligned16(v_sc) && aligned16(beta_sc);
+// The LDS-DMA path addresses a control row as SGPR base + 32-bit lane byte
+// offset (glds_pair): rows of leading dimension `ld` must stay below 2 GiB.
+bool wide_ok(const double* v_sc, const double* beta_sc, int64_t n, int64_t ld = 0) {
+  return (n % kCplWide == 0) && (ld > 0 ? ld : n) < (int64_t{1} << 28) && aligned16(v_sc) &&
+         aligned16(beta_sc);
 }
 
 // Tile-strided grid: one block per tile of kBlock*CPL candidates, at most
@@ -304,7 +307,7 @@ int mpc_rollout_argmin_batched(const mpc_problem_t* problems, const double* incu
     return MPC_ERR_WORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t ld = static_cast<int64_t>(n_problems) * cand_per_problem;
-  const bool wide = wide_ok(v_sc, beta_sc, cand_per_problem);
+  const bool wide = wide_ok(v_sc, beta_sc, cand_per_problem, ld);
   const int64_t tiles = cdiv(cand_per_problem, kBlock * (wide ? kCplWide : 1));
   const int64_t per_robot = std::min<int64_t>(tiles, rollout_blocks(cand_per_problem));
   const dim3 grid(static_cast<unsigned>(per_robot), static_cast<unsigned>(n_problems));
