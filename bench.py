@@ -415,6 +415,7 @@ def main():
     if not args.host_loop and not exchange:
         host_ms = host_latency_pass(ep, pool)
     elapsed = main_run["elapsed"]
+    chain_step = getattr(ep, "chain", False) and inputs == "resident"
     bytes_launch = 16.0 * n_steps * ep.n_local
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     value = n_total * args.steps / elapsed
@@ -443,13 +444,16 @@ def main():
                                                             if exchange else ""))
                               if use_graph else "eager"),
                    "step_launches": (("chained: rollout of step k + completion of step k-1 in "
-                                      "one launch" + (" (+ local finalize + all_gather)"
-                                                      if exchange else ""))
-                                     if getattr(ep, "chain", False) and inputs == "resident"
+                                      "one launch" + (" (selection over the gathered candidates "
+                                                      "of step k-1; the launch also collects "
+                                                      "this rank's candidate of step k), then "
+                                                      "the all_gather" if exchange else ""))
+                                     if chain_step
                                      else "rollout, then selection" + (
                                          " + all_gather + advance" if exchange else "")),
-                   "parallelism": f"candidate-sharded x{world}" + (", all_gather(808 B)/step"
-                                                                   if exchange else "")},
+                   "parallelism": f"candidate-sharded x{world}" + (
+                       (", all_gather(536 B candidates)/step" if chain_step
+                        else ", all_gather(808 B)/step") if exchange else "")},
         "p50_ms": main_run["p50_ms"], "p90_ms": main_run["p90_ms"],
         "p50_note": "GPU time per MPC step (HIP events between step starts, eager launches)",
         "p50_host_ms": percentile(host_ms, 50) if host_ms else None,
@@ -708,8 +712,8 @@ def kernel_pass(ep, pool, reps=100, warm=200):
     return k0.elapsed_time(k1) / reps
 
 
-TRAFFIC_JSON = {"k_rollout_argmin_stream": "r02_traffic.json",
-                "k_episode_chain": "r02_traffic_chain.json"}
+TRAFFIC_JSON = {"k_rollout_argmin_stream": "r03_traffic_stream.json",
+                "k_episode_chain": "r03_traffic_chain.json"}
 
 # fp64 VALU counters (tools/pmc_valu.sh: SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F64,
 # SQ_INSTS_VALU) of each kernel at the size it was measured on:

@@ -632,9 +632,15 @@ __device__ void collect_local_candidate(const Rec* __restrict__ part, int n_part
     for (int q = 0; q < 8; ++q) {
       const uint32_t lo = static_cast<uint32_t>(r[q].y);
       const int64_t idx = lo == 0xffffffffu ? INT64_MAX : static_cast<int64_t>(lo);
-      if (threadIdx.x + q * kBlock < n_part && rec_less(r[q].x, idx, k, i)) {
-        k = r[q].x;
-        i = idx;
+      if (threadIdx.x + q * kBlock < n_part) {
+        if (rec_less(r[q].x, idx, k, i)) {
+          k = r[q].x;
+          i = idx;
+        }
+        // consumed: untag it.  A replayed HIP graph repeats its launches'
+        // epochs, so a record left tagged would pass for the replay's own
+        // before that launch's tile block stores it.
+        const_cast<Rec*>(ptr[q])->idx = 0;
       }
     }
   } else if (threadIdx.x == 0) {

@@ -799,21 +799,26 @@ def test_chained_wheelbase_mismatch_is_flagged(engine):
     assert ep.chain_error() == 2
 
 
-@pytest.mark.parametrize("wheelbase", [0.5, 0.45])
-def test_chained_exchange_path_and_graph_capture(engine, wheelbase):
+@pytest.mark.parametrize("wheelbase,n,cap", [(0.5, 40_000, 6), (0.45, 40_000, 6),
+                                             (0.5, 1_000_000, 1)])
+def test_chained_exchange_path_and_graph_capture(engine, wheelbase, n, cap):
     """The chained multi-GPU step (launch: rollout of step k + selection over
     step k-1's gathered winners; then step k's local finalize and the RCCL
     all_gather) over a 1-rank nccl group, eager and graph-captured, logs the
-    steps of the single-GPU episode; both wheelbase forms."""
+    steps of the single-GPU episode; both wheelbase forms.  The graph (CAP
+    captured steps) is replayed three times: a replay repeats its launches'
+    epochs, so with one captured step the next replay passes only if no tagged
+    record of the last one survives its consumption."""
     import torch.distributed as dist
     from diplomjourney_amd import math_model_tree as mmt
     from diplomjourney_amd.episode import DeviceEpisode
-    n, ns, steps = 40_000, 10, 12
+    ns, steps = 10, 12
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
     pool = [engine.sample_controls(V, B, n, ns, 900 + i) for i in range(steps)]
+    half, reps = steps - cap, 3
     ref = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64, L=wheelbase)
-    for i in range(steps):
+    for i in list(range(steps)) + list(range(half, steps)) * (reps - 1):
         ref.step(controls=pool[i])
     want = _episode_log(ref)
     own = not dist.is_initialized()
@@ -827,7 +832,6 @@ def test_chained_exchange_path_and_graph_capture(engine, wheelbase):
     try:
         ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64,
                            exchange=True, chain=True, L=wheelbase)
-        half = steps // 2
         for i in range(half):
             ep.step(controls=pool[i])
         ep.flush()
@@ -839,8 +843,9 @@ def test_chained_exchange_path_and_graph_capture(engine, wheelbase):
                 ep.step(controls=pool[i])
             ep.flush()
         ep.steps_enqueued = n0
-        g.replay()
-        ep.steps_enqueued += steps - half
+        for _ in range(reps):
+            g.replay()
+            ep.steps_enqueued += steps - half
         assert _episode_log(ep) == want
         assert ep.chain_error() == 0
     finally:
