@@ -262,16 +262,47 @@ __device__ __forceinline__ bool rec_less(uint64_t ka, int64_t ia, uint64_t kb, i
   return ka < kb || (ka == kb && ia < ib);
 }
 
+// One level of the wave reduction: every lane combines its (key, index) with
+// the lane the DPP pattern CTRL names.  DPP moves run on the VALU: a level is
+// a few cycles instead of an LDS round trip per 32-bit half (ds_bpermute).
+// Lanes of rows outside RM receive an undefined value (no copy of the old
+// one): the reduction below reads only lane 63, whose inputs are all defined.
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ void argmin_dpp_level(uint64_t& k, int64_t& i) {
+  auto mv = [](uint64_t x) {
+    const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(x), CTRL, RM, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(x >> 32), CTRL, RM, 0xf, true);
+    return (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo);
+  };
+  const uint64_t ok = mv(k);
+  const int64_t oi = static_cast<int64_t>(mv(static_cast<uint64_t>(i)));
+  const bool lt = rec_less(ok, oi, k, i);
+  k = lt ? ok : k;
+  i = lt ? oi : i;
+}
+
+// Lexicographic (key, index) minimum over the 64 lanes of a wave (all lanes
+// active), returned in every lane.  quad_perm [1,0,3,2] and [2,3,0,1], then
+// row_half_mirror and row_mirror leave each row of 16 lanes holding its
+// minimum in every lane; row_bcast:15 (into rows 1, 3: lane 31 then holds
+// rows 0-1, lane 63 rows 2-3) and row_bcast:31 (lane 31 into row 3) fold the
+// rows into lane 63, which is broadcast.  The minimum of a total order does
+// not depend on the combination order: the same result as any other
+// reduction tree.
 __device__ __forceinline__ void wave_argmin(uint64_t& k, int64_t& i) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const uint64_t ok = __shfl_xor(k, off, 64);
-    const int64_t oi = __shfl_xor(i, off, 64);
-    if (rec_less(ok, oi, k, i)) {
-      k = ok;
-      i = oi;
-    }
-  }
+  argmin_dpp_level<0xB1>(k, i);
+  argmin_dpp_level<0x4E>(k, i);
+  argmin_dpp_level<0x141>(k, i);
+  argmin_dpp_level<0x140>(k, i);
+  argmin_dpp_level<0x142, 0xA>(k, i);
+  argmin_dpp_level<0x143, 0xC>(k, i);
+  auto lane63 = [](uint64_t x) {
+    const uint32_t lo = __builtin_amdgcn_readlane(static_cast<int>(x), 63);
+    const uint32_t hi = __builtin_amdgcn_readlane(static_cast<int>(x >> 32), 63);
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+  };
+  k = lane63(k);
+  i = static_cast<int64_t>(lane63(static_cast<uint64_t>(i)));
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
