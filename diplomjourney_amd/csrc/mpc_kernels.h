@@ -546,7 +546,7 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
   // Regular pass (step_core's forms and range checks), then — if any step is
   // irregular — the safe pass (step_safe's forms) for the whole candidate,
   // exactly as rollout_candidate / the rollout kernels decide.
-  double vs = 0.0, w = 0.0, bs = 0.0;
+  double vs = 0.0, w = 0.0, bs = 0.0, d = 0.0, ra = 0.0, rc = 0.0;
   if (valid && lane < n_steps) {
     // pre_v / pre_b: the winner's controls already staged in LDS by the caller
     // (finalize_block prefetches each wave's best during the block reduction)
@@ -555,14 +555,18 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
     s_v[lane] = vs;
     if (lane == 0) s_b0 = bs;
     w = K.L_pow2 ? vs * K.inv_L : vs / K.L;
-    const double d = heading_incr<INTEG>(w, trig::tan_small(bs), K);
+    d = heading_incr<INTEG>(w, trig::tan_small(bs), K);
     s_dphi[lane] = d;
     const bool lane_bad =
         !(fabs(bs) <= trig::kTanMax) || (ROT && !(fabs(d) <= trig::kRotMax));
     if (lane_bad) s_bad = 1;
     // rotation mode: the factors depend on this step's increment only, so
     // they are formed here, in the same phase (no heading chain needed)
-    if (ROT && !lane_bad) trig::rotation_factors(d, s_a[lane], s_c[lane]);
+    if (ROT && !lane_bad) {
+      trig::rotation_factors(d, ra, rc);
+      s_a[lane] = ra;
+      s_c[lane] = rc;
+    }
   }
   __syncthreads();
   // Regular rotation-mode winner: ONE serial pass on lane 0 (heading, rotation,
@@ -633,17 +637,28 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
         step_start<ROT>(K, x, y, ph, sn, cs);    // kRotCum: identity rotation, empty sums
       else
         step_start<0>(K, x, y, ph, sn, cs);
+      // the fast pass takes step st's values from lane st's registers
+      // (v_readlane: no LDS round trip per step on the serial path)
+      auto rl = [](double val, int src) {
+        const uint64_t u = static_cast<uint64_t>(__double_as_longlong(val));
+        const uint32_t lo = __builtin_amdgcn_readlane(static_cast<int>(u), src);
+        const uint32_t hi = __builtin_amdgcn_readlane(static_cast<int>(u >> 32), src);
+        return __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | lo));
+      };
       for (int st = 0; st < n_steps; ++st) {
+        double vst;
         if (fast) {
-          ph = ph + s_dphi[st];
-          trig::rotate_by(s_a[st], s_c[st], sn, cs);
+          ph = ph + rl(d, st);
+          trig::rotate_by(rl(ra, st), rl(rc, st), sn, cs);
+          vst = rl(vs, st);
         } else {
           ph = s_phi[st];
           sn = s_a[st];
           cs = s_c[st];
+          vst = s_v[st];
         }
-        x = position_step<INTEG>(x, s_v[st], cs, K);
-        y = position_step<INTEG>(y, s_v[st], sn, K);
+        x = position_step<INTEG>(x, vst, cs, K);
+        y = position_step<INTEG>(y, vst, sn, K);
         double px = x, py = y;
         if (ROT == kRotCum && fast) cum_pose(K, x, y, px, py);
         s_tr[3 * st] = px;

@@ -1,0 +1,153 @@
+"""Per-block timeline of the chained step (k_episode_chain): a variant build of
+the library with s_memrealtime (100 MHz) stamps patched into a copy of the
+sources (the shipped sources carry none), then one chained step among
+back-to-back ones, decoded per phase.
+
+    python tools/chain_timeline.py build            # -> tools/var_timeline.so (CPU)
+    python tools/chain_timeline.py run N_CAND N     # on the GPU box
+
+Block 0 (completion of step k-1): entry, records loaded + lane minima, wave
+arg-min, block winner (after the barrier), winner re-rolled (emit_winner),
+episode updated (thread 0), head stored + constants published.
+Tile blocks: entry, first control DMAs in flight (pre0), final constants in
+hand (after the loop), record stored."""
+import ctypes
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VAR = os.path.join(REPO, "tools", "var_timeline.so")
+NB = 2048 + 1
+B0 = ["entry", "records", "wave argmin", "block winner", "controls in LDS", "re-roll",
+      "advance", "update", "published"]
+B0_BASE = 8 * NB   # block 0's stamps follow the tiles' (8 per block)
+TILE = ["entry", "DMAs issued", "final consts", "record stored"]
+
+STAMP = "__hip_atomic_store(&g_tl[{slot}], __builtin_amdgcn_s_memrealtime(), " \
+        "__ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)"
+
+
+def patch(path, edits):
+    s = open(path).read()
+    for anchor, new in edits:
+        if s.count(anchor) != 1:
+            raise SystemExit(f"{os.path.basename(path)}: anchor found {s.count(anchor)}x: {anchor!r}")
+        s = s.replace(anchor, new)
+    open(path, "w").write(s)
+
+
+def build():
+    d = tempfile.mkdtemp()
+    shutil.copytree(os.path.join(REPO, "include"), os.path.join(d, "include"))
+    shutil.copytree(os.path.join(REPO, "diplomjourney_amd", "csrc"),
+                    os.path.join(d, "diplomjourney_amd", "csrc"))
+    cs = os.path.join(d, "diplomjourney_amd", "csrc")
+    st = lambda slot: STAMP.format(slot=slot)   # noqa: E731
+    b0 = lambda q: f"if (blockIdx.x == 0 && threadIdx.x == 0) {st(B0_BASE + q)};"   # noqa: E731
+    patch(os.path.join(cs, "mpc_kernels.h"), [
+        ("struct Rec {\n", f"__device__ uint64_t g_tl[8 * {NB} + 16];\n\nstruct Rec {{\n"),
+        ("  if (KDEV && hook.H && threadIdx.x >= 64 && threadIdx.x < 64 + kStagedWords)\n"
+         "    s_head[threadIdx.x - 64]",
+         f"  {b0(1)}\n"
+         "  if (KDEV && hook.H && threadIdx.x >= 64 && threadIdx.x < 64 + kStagedWords)\n"
+         "    s_head[threadIdx.x - 64]"),
+        ("  wave_argmin(k, i);\n  // Each wave's best", f"  wave_argmin(k, i);\n  {b0(2)}\n  // Each wave's best"),
+        ("  int wbest = 0;\n", f"  {b0(3)}\n  int wbest = 0;\n"),
+        ("  if (KDEV && hook.H) {\n    if (threadIdx.x == 0) {   // emit_winner ended with a barrier\n",
+         f"  {b0(5)}\n  if (KDEV && hook.H) {{\n    if (threadIdx.x == 0) {{   // emit_winner ended with a barrier\n"),
+        ("      __builtin_memcpy(s_head, &H, sizeof(EpisodeHead));\n    }\n    __syncthreads();\n"
+         "    // the head and the log record back to HBM, the chain tags cleared\n",
+         f"      __builtin_memcpy(s_head, &H, sizeof(EpisodeHead));\n      {b0(7)}\n    }}\n"
+         "    __syncthreads();\n"
+         "    // the head and the log record back to HBM, the chain tags cleared\n"),
+        ("                 hook.chain_pub, hook.chain_pub_words, hook.publish_epoch);\n  }\n}\n",
+         "                 hook.chain_pub, hook.chain_pub_words, hook.publish_epoch);\n"
+         f"    {b0(8)}\n  }}\n}}\n"),
+        ("  __syncthreads();\n  // Regular rotation-mode winner",
+         f"  __syncthreads();\n  {b0(4)}\n  // Regular rotation-mode winner"),
+    ])
+    t = lambda q: f"if (threadIdx.x == 0) {STAMP.format(slot=f'8 * blockIdx.x + {q}')};"   # noqa: E731
+    patch(os.path.join(cs, "mpc_episode.h"), [
+        ("  L.status = status;\n  if (ended) episode_restart(c, *S);\n",
+         f"  L.status = status;\n  {b0(6)}\n  if (ended) episode_restart(c, *S);\n"),
+        ("  if (blockIdx.x == 0) {\n    if (has_prev) {\n",
+         f"  if (blockIdx.x == 0) {{\n    {t(0)}\n    if (has_prev) {{\n"),
+        ("  constexpr int CPL = 2;\n  __shared__ uint32_t s_w[kPubWords], s_tag[kPubWords];\n",
+         f"  {t(0)}\n  constexpr int CPL = 2;\n  __shared__ uint32_t s_w[kPubWords], s_tag[kPubWords];\n"),
+        ("      if (threadIdx.x == 0) s_final = fin;\n    }\n    __syncthreads();\n",
+         f"      if (threadIdx.x == 0) s_final = fin;\n    }}\n    __syncthreads();\n    {t(1)}\n"),
+        ("    K = consts_from_words(s_w);\n  };\n", f"    K = consts_from_words(s_w);\n    {t(2)}\n  }};\n"),
+        ("    else\n      part[blockIdx.x - 1] = Rec{best_k, best_i};\n  }\n}\n",
+         "    else\n      part[blockIdx.x - 1] = Rec{best_k, best_i};\n"
+         f"    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    {t(3)}\n  }}\n}}\n"),
+    ])
+    patch(os.path.join(cs, "mpc_rollout.hip"), [
+        ("// ----------------------------- RCCL exchange",
+         "extern \"C\" int mpc_debug_timeline(void* dst, size_t bytes) {\n"
+         "  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(mpc::g_tl), bytes) == hipSuccess ? 0 : -1;\n"
+         "}\n\n// ----------------------------- RCCL exchange"),
+    ])
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-ldl", "-ffp-contract=off", "-I", os.path.join(d, "include"), "-o", VAR,
+           os.path.join(cs, "mpc_rollout.hip")]
+    r = subprocess.run(cmd, capture_output=True, text=True, cwd=d)
+    shutil.rmtree(d)
+    if r.returncode:
+        raise SystemExit(r.stderr[-3000:])
+    print(VAR)
+
+
+def run(n, ns):
+    os.environ["DIPLOMJOURNEY_MPC_LIB"] = VAR
+    sys.path.insert(0, REPO)
+    import torch
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd import native
+    from diplomjourney_amd.episode import DeviceEpisode
+    from diplomjourney_amd.expansion import Expansion
+    eng = Expansion("cuda:0")
+    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
+    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
+    pool = [eng.sample_controls(V, B, n, ns, 0x5EED0000 + i) for i in range(8)]
+    ep = DeviceEpisode(eng, n, ns, integrator="rect+cum", chain=True, log_capacity=8192)
+    L = native.lib()
+    L.mpc_debug_timeline.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    nb = (n + 511) // 512 + 1
+    buf = (ctypes.c_uint64 * (8 * NB + 16))()
+    rows = []
+    for rep in range(5):
+        for i in range(300):
+            ep.step(controls=pool[i % 8])
+        torch.cuda.synchronize()
+        assert L.mpc_debug_timeline(buf, ctypes.sizeof(buf)) == 0
+        t = [buf[j] for j in range(8 * nb)]
+        t0 = min(t[8 * b] for b in range(nb))
+        us = lambda x: (x - t0) * 0.01   # noqa: E731
+        b0 = {"entry": us(t[0])}
+        b0.update({name: us(buf[B0_BASE + q]) for q, name in enumerate(B0) if q})
+        row = {"block0": b0}
+        for q, name in enumerate(TILE):
+            xs = sorted(us(t[8 * b + q]) for b in range(1, nb))
+            row[name] = [xs[int(p * (len(xs) - 1))] for p in (0.1, 0.5, 0.9)] + [xs[-1]]
+        rows.append(row)
+    ep.flush()
+    assert ep.chain_error() == 0
+    print(f"chained step, {n} candidates, N = {ns}, {nb} blocks; us after the first block's entry")
+    for r in rows:
+        b0 = r["block0"]
+        print("  block 0: " + "  ".join(f"{k} {v:5.2f}" for k, v in b0.items()))
+        print("  tiles p10/p50/p90/max: " + "  ".join(
+            f"{k} " + "/".join(f"{x:.2f}" for x in r[k]) for k in TILE))
+    print("JSON " + json.dumps(rows))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build()
+    else:
+        run(int(sys.argv[2]), int(sys.argv[3]))
