@@ -527,7 +527,7 @@ __device__ void advance_from_candidates(const mpc_episode_config_t& c, EpisodeSt
                                         const mpc_candidate_t* __restrict__ g, int n,
                                         mpc_result_t* __restrict__ out,
                                         mpc_episode_log_t* __restrict__ log, int cap,
-                                        uint32_t publish_epoch) {
+                                        uint32_t publish_epoch, EmitLds* lds) {
   __shared__ uint64_t s_head[kStagedWords];
   __shared__ mpc_episode_log_t s_log;
   __shared__ mpc_episode_log_t* s_slot;
@@ -557,7 +557,7 @@ __device__ void advance_from_candidates(const mpc_episode_config_t& c, EpisodeSt
   const Consts K = Hs->K;                // the step's constants (before the update)
   Winner win;
   emit_winner<INTEG, ROT>(K, nullptr, nullptr, 0, w->n_steps, s_bk, 0, w->index, Hs->incumbent,
-                          out, &win, w->v, w->beta);
+                          out, lds, &win, w->v, w->beta, true);
   if (threadIdx.x == 0) {   // emit_winner ended with a barrier; lane 0 holds `win`
     EpisodeHead H;
     __builtin_memcpy(&H, s_head, sizeof(EpisodeHead));
@@ -570,13 +570,15 @@ __device__ void advance_from_candidates(const mpc_episode_config_t& c, EpisodeSt
   // publishes the next step's constants (a chained exchange step's block 0)
   store_update(&S->h, s_head, s_slot, reinterpret_cast<const uint64_t*>(&s_log), S->chain_pub,
                kPubWords, publish_epoch);
+  emit_winner_tail<INTEG, ROT>(K, w->n_steps, lds, out);   // the rest of the record
 }
 
 template <int INTEG, int ROT>
 __global__ __launch_bounds__(kFinBlock) void k_episode_advance_cand(
     mpc_episode_config_t c, EpisodeState* __restrict__ S, const mpc_candidate_t* __restrict__ g,
     int n, mpc_result_t* __restrict__ out, mpc_episode_log_t* __restrict__ log, int cap) {
-  advance_from_candidates<INTEG, ROT>(c, S, g, n, out, log, cap, 0u);
+  __shared__ EmitLds lds;
+  advance_from_candidates<INTEG, ROT>(c, S, g, n, out, log, cap, 0u, &lds);
 }
 
 // A tile block's record in an exchange step: ONE 16-B `sc1` store {cost key,
@@ -771,13 +773,20 @@ __device__ __forceinline__ bool chain_read(const EpisodeState* S, uint32_t epoch
   return __ballot(!ok) == 0;
 }
 
-constexpr int kChainWaves = 5;   // launch bound of the chained kernel: waves per SIMD
+// Launch bound of the chained kernel (waves per SIMD).  The one-GPU form fits
+// 6 (80 VGPRs, no scratch; its LDS fits 6 blocks per CU since block 0's
+// re-roll borrows the idle control ring); the exchange form spills at 6 and
+// runs 5 (measured: the 6-wave build's exchange step was ~0.9 us slower).
+template <int MODE>
+constexpr int chain_waves() {
+  return MODE == kChainFin ? 6 : 5;
+}
 
 // PL2 (wheelbase a power of two) is a template parameter, not a runtime
 // branch: with both rollout variants inlined the kernel held 119 VGPRs and
 // spilled 191 SGPRs; one variant per instantiation: 108-112 VGPRs, 81-86.
 template <int INTEG, int ROT, int MODE, bool PL2>
-__global__ __launch_bounds__(kBlock, kChainWaves) void k_episode_chain(
+__global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
     EpisodeState* __restrict__ S, uint32_t epoch, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part,
     int has_prev, const Rec* __restrict__ part_prev, int n_part_prev,
@@ -792,12 +801,14 @@ __global__ __launch_bounds__(kBlock, kChainWaves) void k_episode_chain(
       if constexpr (MODE == kChainFin) {
         const Consts Kp = S->h.K;
         const EpisodeHook hook{&S->h, log, cap, S->chain_pub, kPubWords, epoch};
+        // (block 0 never fills the control ring: its LDS holds the re-roll)
         finalize_block<INTEG, ROT, true, kBlock, false>(part_prev, n_part_prev, Kp, v_prev,
                                                         b_prev, n_cand, n_steps, index_base,
-                                                        S->h.incumbent, out_prev, ecfg, hook);
+                                                        S->h.incumbent, out_prev, ecfg, hook,
+                                                        ring_lds());
       } else {
         advance_from_candidates<INTEG, ROT>(ecfg, S, gathered, n_gathered, out_prev, log, cap,
-                                            epoch);
+                                            epoch, ring_lds());
       }
       __syncthreads();   // (the wheelbase check below reads the stored head)
     } else {
@@ -888,21 +899,25 @@ __global__ __launch_bounds__(kBlock, kChainWaves) void k_episode_chain(
     }
     K = consts_from_words(s_w);
   };
-  const int64_t n_tiles = (n_cand + kBlock * CPL - 1) / (kBlock * CPL);
+  // 32-bit candidate indices (the aligned path's rows are < 2^28 candidates,
+  // wide_ok): the clamp below is one v_min with a scalar operand, no 64-bit
+  // select holding its own registers across the loop
+  const int32_t n32 = static_cast<int32_t>(n_cand);
+  const int32_t n_tiles = (n32 + kBlock * CPL - 1) / (kBlock * CPL);
   uint64_t best_k = ~0ull;
   int64_t best_i = INT64_MAX;
-  for (int64_t tile = blockIdx.x - 1; tile < n_tiles; tile += gridDim.x - 1) {
-    const int64_t c0 = tile * (kBlock * CPL) + threadIdx.x * CPL;
+  for (int32_t tile = blockIdx.x - 1; tile < n_tiles; tile += gridDim.x - 1) {
+    const int32_t c0 = tile * (kBlock * CPL) + static_cast<int32_t>(threadIdx.x) * CPL;
     // lanes past the end of a partial tile roll the last pair again (result
     // ignored), so every lane reaches the barriers of pre0 / wait on the same path
-    const int64_t cl = c0 < n_cand ? c0 : n_cand - CPL;
+    const int32_t cl = min(c0, n32 - CPL);
     double cst[CPL];
     // leading trig coefficients not pinned: the fifth wave per SIMD needs the
     // registers more (as the rect+cum stream kernel)
     rollout_lane_glds_k<INTEG, ROT, PL2, decltype(wait), decltype(pre0), decltype(mid),
                         false>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0, mid);
     Kl = K;            // later tiles: the final constants
-    if (c0 < n_cand) {
+    if (c0 < n32) {
 #pragma unroll
       for (int j = 0; j < CPL; ++j) {
         const uint64_t kk = cost_key(cst[j]);

@@ -520,14 +520,38 @@ struct Winner {
 // x and y.  The winner is regular or irregular exactly as in rollout_lane
 // (same tests), and each branch repeats that path's operations in the same
 // order, so the emitted states are bitwise those the arg-min scored.
+// LDS of the winner's re-roll (emit_winner) and of the selection's staged
+// controls (finalize_block), provided by the caller: a kernel that owns LDS
+// it is not using at that point — the chained step's block 0 and the fused
+// finalize have the control ring — lends that instead of adding 2.5 KiB to
+// the kernel's LDS (which decides how many blocks fit on a CU).
+struct EmitLds {
+  double v[MPC_MAX_STEPS], dphi[MPC_MAX_STEPS], phi[MPC_MAX_STEPS];
+  double a[MPC_MAX_STEPS], c[MPC_MAX_STEPS];
+  double tr[MPC_MAX_STEPS * 3];
+  double pv[MPC_MAX_STEPS], pb[MPC_MAX_STEPS];
+  double tail[5];      // deferred re-roll: lane 0's state (x, y, sin, cos, phi) ...
+  int tail_from;       // ... after this many steps (== n_steps: nothing deferred)
+};
+
+// The control ring's LDS lent to the re-roll (a block whose ring is idle).
+__device__ __forceinline__ EmitLds* ring_lds() {
+  static_assert(sizeof(EmitLds) <= sizeof(g_ring), "the re-roll's LDS fits in the ring");
+  return reinterpret_cast<EmitLds*>(&g_ring[0][0][0][0]);
+}
+
 template <int INTEG, int ROT>
 __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
                             const double* __restrict__ b, int64_t ld, int n_steps, uint64_t key,
                             int64_t col, int64_t reported_index, double incumbent,
-                            mpc_result_t* __restrict__ out, Winner* win = nullptr,
-                            const double* pre_v = nullptr, const double* pre_b = nullptr) {
-  __shared__ double s_v[MPC_MAX_STEPS], s_dphi[MPC_MAX_STEPS], s_phi[MPC_MAX_STEPS];
-  __shared__ double s_a[MPC_MAX_STEPS], s_c[MPC_MAX_STEPS];
+                            mpc_result_t* __restrict__ out, EmitLds* lds, Winner* win = nullptr,
+                            const double* pre_v = nullptr, const double* pre_b = nullptr,
+                            bool defer_tail = false) {
+  double* s_v = lds->v;
+  double* s_dphi = lds->dphi;
+  double* s_phi = lds->phi;
+  double* s_a = lds->a;
+  double* s_c = lds->c;
   __shared__ double s_b0;
   __shared__ uint64_t s_key;
   __shared__ int64_t s_col, s_rep;
@@ -602,8 +626,14 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
   // Lane 0 runs the serial pass into LDS; the record's trajectory is then
   // stored by one lane per value (a single lane's ~30 stores would serialise
   // in the address path for ~1 us).
-  __shared__ double s_tr[MPC_MAX_STEPS * 3];
+  // defer_tail (a regular rotation-mode winner): the pass stops after the
+  // three layer states the episode update needs; emit_winner_tail() finishes
+  // the record's trajectory once the update is out (same operations, same
+  // order, continued from the saved state).
+  double* s_tr = lds->tr;
+  const int n_run = (defer_tail && fast && n_steps > 3) ? 3 : n_steps;
   if (lane == 0) {
+    lds->tail_from = n_steps;
     out->n_steps = n_steps;
     if (win) win->n_steps = n_steps;
     if (!valid) {
@@ -645,7 +675,7 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
         const uint32_t hi = __builtin_amdgcn_readlane(static_cast<int>(u >> 32), src);
         return __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | lo));
       };
-      for (int st = 0; st < n_steps; ++st) {
+      for (int st = 0; st < n_run; ++st) {
         double vst;
         if (fast) {
           ph = ph + rl(d, st);
@@ -670,10 +700,46 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
           win->tr[st][2] = ph;
         }
       }
+      if (n_run < n_steps) {
+        lds->tail[0] = x;
+        lds->tail[1] = y;
+        lds->tail[2] = sn;
+        lds->tail[3] = cs;
+        lds->tail[4] = ph;
+        lds->tail_from = n_run;
+      }
     }
   }
   __syncthreads();
-  if (valid && lane < 3 * n_steps) (&out->traj[0][0])[lane] = s_tr[lane];
+  if (valid && lane < 3 * lds->tail_from) (&out->traj[0][0])[lane] = s_tr[lane];
+}
+
+// The rest of a deferred re-roll (emit_winner with defer_tail): every thread,
+// after a barrier that follows emit_winner; K = the constants it was given.
+template <int INTEG, int ROT>
+__device__ void emit_winner_tail(const Consts& K, int n_steps, EmitLds* lds,
+                                 mpc_result_t* __restrict__ out) {
+  const int from = lds->tail_from;   // uniform
+  if (from >= n_steps) return;
+  double* s_tr = lds->tr;
+  if (threadIdx.x == 0) {
+    double x = lds->tail[0], y = lds->tail[1], sn = lds->tail[2], cs = lds->tail[3],
+           ph = lds->tail[4];
+    for (int st = from; st < n_steps; ++st) {
+      ph = ph + lds->dphi[st];
+      trig::rotate_by(lds->a[st], lds->c[st], sn, cs);
+      x = position_step<INTEG>(x, lds->v[st], cs, K);
+      y = position_step<INTEG>(y, lds->v[st], sn, K);
+      double px = x, py = y;
+      if (ROT == kRotCum) cum_pose(K, x, y, px, py);
+      s_tr[3 * st] = px;
+      s_tr[3 * st + 1] = py;
+      s_tr[3 * st + 2] = ph;
+    }
+  }
+  __syncthreads();
+  const int q = threadIdx.x;
+  if (q >= 3 * from && q < 3 * n_steps) (&out->traj[0][0])[q] = s_tr[q];
 }
 
 // The device-resident episode's scalars (mpc_episode.h: EpisodeState = this
@@ -793,7 +859,7 @@ __device__ __forceinline__ void finalize_block(
     const Rec* __restrict__ part, int n_part, const Consts& K, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, int64_t index_base,
     double incumbent, mpc_result_t* __restrict__ out, const mpc_episode_config_t& ecfg,
-    const EpisodeHook& hook) {
+    const EpisodeHook& hook, EmitLds* lds) {
   // One-GPU episode: the episode scalars are staged in LDS by wave 1 (one
   // 8-B vector load per lane, issued after its record loads) and updated by
   // thread 0 once the winner is known.  (Loading them into thread 0's SGPRs
@@ -850,7 +916,8 @@ __device__ __forceinline__ void finalize_block(
   // combined: the block's winner is one of them, so its re-roll starts
   // without a dependent load of its own (one memory round trip fewer on the
   // selection's critical path; the same values, so the same arithmetic).
-  __shared__ double s_pv[MPC_MAX_STEPS], s_pb[MPC_MAX_STEPS];
+  double* s_pv = lds->pv;
+  double* s_pb = lds->pb;
   double pv = 0.0, pb = 0.0;
   const int ln = threadIdx.x & 63;
   if constexpr (!GEN) {
@@ -886,10 +953,10 @@ __device__ __forceinline__ void finalize_block(
     // (thread 0 holds the winner; emit_winner takes its column from thread 0)
     // (k_rollout_generated: 2 candidates per lane, tiles dealt round-robin)
     const int64_t col = k == ~0ull ? 0 : ((i / (kBlock * 2)) % n_part) * MPC_MAX_STEPS;
-    emit_winner<INTEG, ROT>(K, v, b, 1, n_steps, k, col, index_base + i, incumbent, out, &w);
+    emit_winner<INTEG, ROT>(K, v, b, 1, n_steps, k, col, index_base + i, incumbent, out, lds, &w);
   } else {
-    emit_winner<INTEG, ROT>(K, v, b, n_cand, n_steps, k, i, index_base + i, incumbent, out, &w,
-                            s_pv, s_pb);
+    emit_winner<INTEG, ROT>(K, v, b, n_cand, n_steps, k, i, index_base + i, incumbent, out, lds,
+                            &w, s_pv, s_pb, KDEV && hook.H);
   }
   if (KDEV && hook.H) {
     if (threadIdx.x == 0) {   // emit_winner ended with a barrier
@@ -903,6 +970,8 @@ __device__ __forceinline__ void finalize_block(
     // the head and the log record back to HBM, the chain tags cleared
     store_update(hook.H, s_head, s_slot, reinterpret_cast<const uint64_t*>(&s_log),
                  hook.chain_pub, hook.chain_pub_words, hook.publish_epoch);
+    // the record's remaining trajectory, off the update's critical path
+    emit_winner_tail<INTEG, ROT>(K, n_steps, lds, out);
   }
 }
 
@@ -914,9 +983,10 @@ __global__ __launch_bounds__(kFinBlock) void k_finalize_gen(
     int64_t index_base, const double* __restrict__ incumbent_dev,
     mpc_result_t* __restrict__ out, mpc_episode_config_t ecfg, EpisodeHook hook) {
   const Consts K = *Kdev;
+  __shared__ EmitLds lds;
   finalize_block<INTEG, ROT, true, kFinBlock, false, true>(part, n_part, K, part_v, part_b, 0,
                                                            n_steps, index_base, *incumbent_dev,
-                                                           out, ecfg, hook);
+                                                           out, ecfg, hook, &lds);
 }
 
 template <int INTEG, int ROT, bool KDEV>
@@ -927,8 +997,9 @@ __global__ __launch_bounds__(kFinBlock) void k_finalize(
     mpc_result_t* __restrict__ out, mpc_episode_config_t ecfg, EpisodeHook hook) {
   const Consts K = KDEV ? *Kdev : Karg;
   const double incumbent = KDEV ? *incumbent_dev : incumbent_arg;
+  __shared__ EmitLds lds;
   finalize_block<INTEG, ROT, KDEV, kFinBlock, false>(part, n_part, K, v, b, n_cand, n_steps,
-                                                     index_base, incumbent, out, ecfg, hook);
+                                                     index_base, incumbent, out, ecfg, hook, &lds);
 }
 
 // Device-resident episode, one launch per MPC step: the streaming rollout +
@@ -979,8 +1050,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_rollout_episode(
   }
   __syncthreads();
   if (!s_last) return;
+  // (the block's control ring is drained: its LDS holds the re-roll)
   finalize_block<INTEG, ROT, true, kBlock, true>(part, gridDim.x, K, v, b, n_cand, n_steps,
-                                                 index_base, *incumbent_dev, out, ecfg, hook);
+                                                 index_base, *incumbent_dev, out, ecfg, hook,
+                                                 ring_lds());
   if (threadIdx.x == 0) *done = 0u;
 }
 
@@ -1101,7 +1174,8 @@ __global__ __launch_bounds__(kBlock) void k_finalize_batched(
   block_argmin(k, i);
   const Consts K = consts_from_problem(probs[r]);
   const double inc = incumbents ? incumbents[r] : __builtin_inf();
-  emit_winner<INTEG, ROT>(K, v, b, ld, n_steps, k, r * cand + i, i, inc, &out[r]);
+  __shared__ EmitLds lds;
+  emit_winner<INTEG, ROT>(K, v, b, ld, n_steps, k, r * cand + i, i, inc, &out[r], &lds);
 }
 
 // --------------------------- exchange ----------------------------------------

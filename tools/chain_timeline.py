@@ -65,9 +65,9 @@ def build():
          f"      __builtin_memcpy(s_head, &H, sizeof(EpisodeHead));\n      {b0(7)}\n    }}\n"
          "    __syncthreads();\n"
          "    // the head and the log record back to HBM, the chain tags cleared\n"),
-        ("                 hook.chain_pub, hook.chain_pub_words, hook.publish_epoch);\n  }\n}\n",
+        ("                 hook.chain_pub, hook.chain_pub_words, hook.publish_epoch);\n",
          "                 hook.chain_pub, hook.chain_pub_words, hook.publish_epoch);\n"
-         f"    {b0(8)}\n  }}\n}}\n"),
+         f"    {b0(8)}\n"),
         ("  __syncthreads();\n  // Regular rotation-mode winner",
          f"  __syncthreads();\n  {b0(4)}\n  // Regular rotation-mode winner"),
     ])
