@@ -107,7 +107,13 @@ MPC_HD __forceinline__ double position_step(double p, double v, double trig, con
 //   PL2 + RECT:  (v * inv_L) * h is formed as (v * h) * inv_L — the same
 //                value (scaling by a power of two commutes with rounding in the
 //                normal range) — so v * h is shared with the position update.
+//                kRotCum goes one step further: v * (h * inv_L) serves both, the
+//                sums A, B are accumulated scaled by 1/L (every rounding scales
+//                exactly) and cum_pose<true> scales them back: the same bits
+//                as the unscaled sums, one multiply fewer per step.
 //   ld:          VGPR-resident leading coefficients (trig::Leads), or nullptr.
+constexpr int kRotCum = 2;
+
 template <int INTEG, int ROT, bool PL2>
 MPC_HD __forceinline__ void step_core(double& x, double& y, double& ph, double& s, double& c,
                                       double v, double beta, const Consts& K, bool& bad,
@@ -115,7 +121,10 @@ MPC_HD __forceinline__ void step_core(double& x, double& y, double& ph, double& 
   bad |= !(fabs(beta) <= trig::kTanMax);
   const double t = trig::tan_small(beta, ld);
   double dphi, vh = 0.0;
-  if constexpr (PL2 && INTEG == MPC_INTEG_RECT) {
+  if constexpr (PL2 && INTEG == MPC_INTEG_RECT && ROT == kRotCum) {
+    vh = v * (K.h * K.inv_L);                                  // the sums scaled by 1/L
+    dphi = vh * t;                                             // angle_phi (:107)
+  } else if constexpr (PL2 && INTEG == MPC_INTEG_RECT) {
     vh = v * K.h;
     dphi = (vh * K.inv_L) * t;                                 // angle_phi (:107)
   } else {
@@ -125,9 +134,9 @@ MPC_HD __forceinline__ void step_core(double& x, double& y, double& ph, double& 
   ph = ph + dphi;                                              // phi + _phi      (:113)
   if constexpr (ROT) {
     bad |= !(fabs(dphi) <= trig::kRotMax);
-    double sd, cm1;
-    trig::rotation_factors(dphi, sd, cm1, ld);
-    trig::rotate_by(sd, cm1, s, c);
+    double sd, cd;
+    trig::rotation_sc(dphi, sd, cd, ld);
+    trig::rotate_sc(sd, cd, s, c);
   } else {
     bad |= !(fabs(ph) <= trig::kFastMax);
     trig::sincos_core(ph, &s, &c);
@@ -140,8 +149,6 @@ MPC_HD __forceinline__ void step_core(double& x, double& y, double& ph, double& 
     y = position_step<INTEG>(y, v, s, K);                      // coordinate_y    (:103)
   }
 }
-
-constexpr int kRotCum = 2;
 
 // Start state of the step recurrence: the pose (ROT 0 / 1) or the identity
 // rotation and empty sums (kRotCum).
@@ -162,8 +169,14 @@ MPC_HD __forceinline__ void step_start(const Consts& K, double& x, double& y, do
   }
 }
 
-// kRotCum: position from the sums, x = x0 + (c0 A - s0 B), y = y0 + (s0 A + c0 B)
+// kRotCum: position from the sums, x = x0 + (c0 A - s0 B), y = y0 + (s0 A + c0 B).
+// SCALED: the sums of step_core<RECT, kRotCum, PL2 = true>, i.e. A/L and B/L.
+template <bool SCALED>
 MPC_HD __forceinline__ void cum_pose(const Consts& K, double A, double B, double& x, double& y) {
+  if constexpr (SCALED) {
+    A = A * K.L;
+    B = B * K.L;
+  }
   x = K.x + fma(K.c0, A, -(K.s0 * B));
   y = K.y + fma(K.s0, A, K.c0 * B);
 }
@@ -207,7 +220,7 @@ MPC_HD inline double rollout_candidate_l(const Consts& K, const double* v, const
     step_core<INTEG, ROT, PL2>(x, y, ph, s, c, v[st * ld + col], b[st * ld + col], K, bad);
     if (traj) {
       if constexpr (ROT == kRotCum) {
-        cum_pose(K, x, y, traj[3 * st + 0], traj[3 * st + 1]);
+        cum_pose<PL2>(K, x, y, traj[3 * st + 0], traj[3 * st + 1]);
       } else {
         traj[3 * st + 0] = x;
         traj[3 * st + 1] = y;
@@ -216,7 +229,7 @@ MPC_HD inline double rollout_candidate_l(const Consts& K, const double* v, const
     }
   }
   if constexpr (ROT == kRotCum) {
-    if (!bad) cum_pose(K, x, y, x, y);
+    if (!bad) cum_pose<PL2>(K, x, y, x, y);
   }
   if (bad) {
     x = K.x;

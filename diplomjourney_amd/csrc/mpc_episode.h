@@ -230,7 +230,7 @@ __device__ __forceinline__ void generated_lane(const Consts& K, const double2* s
   if constexpr (ROT == kRotCum) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      if (!bad[j]) cum_pose(K, x[j], y[j], x[j], y[j]);
+      if (!bad[j]) cum_pose<PL2>(K, x[j], y[j], x[j], y[j]);
   }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {

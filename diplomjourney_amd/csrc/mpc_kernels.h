@@ -100,7 +100,7 @@ __device__ __forceinline__ void rollout_lane_l(const Consts& K, const double* __
       step_core<INTEG, ROT, PL2>(x[j], y[j], ph[j], sn[j], cs[j], vv[j], bb[j], K, bad[j]);
       if constexpr (STATES) {
         double px = x[j], py = y[j];
-        if constexpr (ROT == kRotCum) cum_pose(K, x[j], y[j], px, py);
+        if constexpr (ROT == kRotCum) cum_pose<PL2>(K, x[j], y[j], px, py);
         states[(sr * 3 + 0) * n_cand + c0 + j] = px;
         states[(sr * 3 + 1) * n_cand + c0 + j] = py;
         states[(sr * 3 + 2) * n_cand + c0 + j] = ph[j];
@@ -134,7 +134,7 @@ __device__ __forceinline__ void rollout_lane_l(const Consts& K, const double* __
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
     if constexpr (ROT == kRotCum) {
-      if (!bad[j]) cum_pose(K, x[j], y[j], x[j], y[j]);
+      if (!bad[j]) cum_pose<PL2>(K, x[j], y[j], x[j], y[j]);
     }
     if (bad[j]) {
       x[j] = K.x;
@@ -280,7 +280,7 @@ __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Const
   // re-materialised per step)
   trig::Leads lead = trig::const_leads();
   if constexpr (PIN)
-    asm volatile("" : "+v"(lead.tp), "+v"(lead.tq), "+v"(lead.rs), "+v"(lead.rc));
+    asm volatile("" : "+v"(lead.tp), "+v"(lead.rs), "+v"(lead.rc));
   // The loop constants: Kloop (read after pre0), or K when a speculated step
   // size turns out wrong (kRotCum with a real pre(): the chained step after an
   // episode restart) and the loop runs again from the controls with the final
@@ -352,7 +352,7 @@ __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Const
       }
 #pragma unroll
       for (int j = 0; j < CPL; ++j)
-        if (!bad[j]) cum_pose(K, x[j], y[j], x[j], y[j]);
+        if (!bad[j]) cum_pose<PL2>(K, x[j], y[j], x[j], y[j]);
     }
     break;
   }
@@ -587,7 +587,7 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
     // rotation mode: the factors depend on this step's increment only, so
     // they are formed here, in the same phase (no heading chain needed)
     if (ROT && !lane_bad) {
-      trig::rotation_factors(d, ra, rc);
+      trig::rotation_sc(d, ra, rc);
       s_a[lane] = ra;
       s_c[lane] = rc;
     }
@@ -679,7 +679,7 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
         double vst;
         if (fast) {
           ph = ph + rl(d, st);
-          trig::rotate_by(rl(ra, st), rl(rc, st), sn, cs);
+          trig::rotate_sc(rl(ra, st), rl(rc, st), sn, cs);
           vst = rl(vs, st);
         } else {
           ph = s_phi[st];
@@ -690,7 +690,7 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
         x = position_step<INTEG>(x, vst, cs, K);
         y = position_step<INTEG>(y, vst, sn, K);
         double px = x, py = y;
-        if (ROT == kRotCum && fast) cum_pose(K, x, y, px, py);
+        if (ROT == kRotCum && fast) cum_pose<false>(K, x, y, px, py);
         s_tr[3 * st] = px;
         s_tr[3 * st + 1] = py;
         s_tr[3 * st + 2] = ph;
@@ -727,11 +727,11 @@ __device__ void emit_winner_tail(const Consts& K, int n_steps, EmitLds* lds,
            ph = lds->tail[4];
     for (int st = from; st < n_steps; ++st) {
       ph = ph + lds->dphi[st];
-      trig::rotate_by(lds->a[st], lds->c[st], sn, cs);
+      trig::rotate_sc(lds->a[st], lds->c[st], sn, cs);
       x = position_step<INTEG>(x, lds->v[st], cs, K);
       y = position_step<INTEG>(y, lds->v[st], sn, K);
       double px = x, py = y;
-      if (ROT == kRotCum) cum_pose(K, x, y, px, py);
+      if (ROT == kRotCum) cum_pose<false>(K, x, y, px, py);
       s_tr[3 * st] = px;
       s_tr[3 * st + 1] = py;
       s_tr[3 * st + 2] = ph;

@@ -149,38 +149,43 @@ MPC_HD inline double ktan(double x, double y, bool odd) {
 
 // Steering-angle tangent without range reduction, |x| <= kTanMax:
 //   tan(x) = x + x^3 * TP(x^2) / TQ(x^2)
-// (tools/fit_trig.py --tan-rational; rel. error of TP/TQ 2.8e-20).  One
-// reciprocal estimate, one Newton step and one correction of the quotient
-// replace the Cody-Waite reduction and the quadrant/cotangent reconstruction
-// of tan_core: ~17 VALU instead of ~50.  The steering bound of the
+// (tools/fit_trig.py --tan-rational --monic: degrees 3/3, rel. error of P/Q
+// 6.2e-17 with the rounded coefficients).  TQ is monic, so its first Horner
+// step is an add (no constant-bus move for a second coefficient operand).
+// One reciprocal estimate and one Newton step form 1/Q (rounded to nearest:
+// tools/micro/rcp_acc.hip finds no difference from 1/q over 2^30 mantissas,
+// so the host build's 1.0 / q gives the same bits); P * (1/Q) is not
+// corrected further: its rounding enters tan with weight x^3 R / tan <= 0.44.
+// ~14 VALU instead of the ~50 of a Cody-Waite reduction and the
+// quadrant/cotangent reconstruction of tan_core.  The steering bound of the
 // reference's config is 60 deg = 1.047 rad; a larger |beta| makes the
 // candidate irregular (recomputed with tan_fast).
 constexpr double kTanMax = 1.1;
-constexpr double kTP[4] = {-0x1.5a006cab24f4bp-20, 0x1.88ebe003d6902p-12, -0x1.81d5aba9c1240p-6,
-                           0x1.5555555555555p-2};
-constexpr double kTQ[5] = {0x1.61e9925b7b933p-20, -0x1.a739351555585p-12, 0x1.c2364f9313e10p-6,
-                           -0x1.e1f1a9c96dd06p-2, 0x1.0000000000000p+0};
+constexpr double kTP[4] = {0x1.2806dd56192d1p-14, -0x1.e9a6933b8c31cp-1, 0x1.4e67ddcc55034p+6,
+                           -0x1.44bcc514568d3p+10};
+constexpr double kTQ[4] = {0x1.0000000000000p+0, -0x1.7f12a2265b864p+6, 0x1.c462cc7b84963p+10,
+                           -0x1.e71b279e81d3cp+11};   // Q in [-3893, -1530] on |x| <= 1.1
 
 // Leading polynomial coefficients of the hot loop's trig, held in VGPRs by
 // the rollout kernel (one copy per lane instead of a v_mov per use); equal to
 // the constants, so results are bitwise those of the default arguments.
 struct Leads {
-  double tp, tq, rs, rc;
+  double tp, rs, rc;
 };
 
 MPC_HD inline double tan_small(double x, const Leads* ld = nullptr) {
   const double s = x * x;
   const double p = ld ? horner(kTP, s, 0, ld->tp, true) : horner(kTP, s);
-  const double q = ld ? horner(kTQ, s, 0, ld->tq, true) : horner(kTQ, s);   // in [0.59, 1]
+  double q = s + kTQ[1];
+  q = fma_k(q, s, kTQ[2]);
+  q = fma_k(q, s, kTQ[3]);
 #if defined(__HIP_DEVICE_COMPILE__)
   double r = __builtin_amdgcn_rcp(q);
-#else
-  double r = 1.0 / q;
-#endif
   r = fma(r, fma(-q, r, 1.0), r);
-  double R = p * r;
-  R = fma(r, fma(-q, R, p), R);           // quotient correction
-  return fma(x * s, R, x);
+#else
+  const double r = 1.0 / q;
+#endif
+  return fma(x * s, p * r, x);
 }
 
 // Core forms: valid for |x| <= kFastMax only (the caller guarantees it or
@@ -359,14 +364,13 @@ constexpr double kRC[4] = {-0x1.27b71672cf54cp-22, 0x1.a019fd094f3a7p-16, -0x1.6
 // cm1 = z * (-1/2 + z * RC(z)): the -1/2 enters as an fma addend (inline
 // constant), one multiply fewer than -z/2 + z^2 * RC(z); its rounding of
 // -1/2 + z*RC adds at most 2^-54 relative, far below cm1's weight in c'.
+// (The full tree's per-control factors, mpc_fulltree.h.)
 MPC_HD inline void rotation_factors(double d, double& sd, double& cm1,
                                     const Leads* ld = nullptr) {
   const double z = d * d;
   sd = fma(d * z, ld ? horner(kRS, z, 0, ld->rs, true) : horner(kRS, z), d);
   cm1 = z * fma(z, ld ? horner(kRC, z, 0, ld->rc, true) : horner(kRC, z), -0.5);
 }
-
-MPC_HD inline Leads const_leads() { return Leads{kTP[0], kTQ[0], kRS[0], kRC[0]}; }
 
 // (s, c) <- rotation of (s, c) by the angle whose factors are (sd, cm1)
 MPC_HD inline void rotate_by(double sd, double cm1, double& s, double& c) {
@@ -375,6 +379,28 @@ MPC_HD inline void rotate_by(double sd, double cm1, double& s, double& c) {
   s = s1;
   c = c1;
 }
+
+// The candidate rollout's form: sd = sin(d) and cd = cos(d) itself, cd =
+// 1 + z * (-1/2 + z * RC(z)) (same operation count as cm1, the final multiply
+// becomes an fma with the inline constant 1), and the rotation as a plain
+// complex product, s' = s*cd + c*sd, c' = c*cd - s*sd: 4 VALU instead of 6.
+// cd's rounding (<= 2^-53 absolute) costs about one ulp of (s, c) per step,
+// ~1e-15 relative over the horizon; the rollout's results are pinned by its
+// host replica (same functions) and against the oracle within 1e-13.
+MPC_HD inline void rotation_sc(double d, double& sd, double& cd, const Leads* ld = nullptr) {
+  const double z = d * d;
+  sd = fma(d * z, ld ? horner(kRS, z, 0, ld->rs, true) : horner(kRS, z), d);
+  cd = fma(z, fma(z, ld ? horner(kRC, z, 0, ld->rc, true) : horner(kRC, z), -0.5), 1.0);
+}
+
+MPC_HD inline void rotate_sc(double sd, double cd, double& s, double& c) {
+  const double s1 = fma(c, sd, s * cd);
+  const double c1 = fma(-s, sd, c * cd);
+  s = s1;
+  c = c1;
+}
+
+MPC_HD inline Leads const_leads() { return Leads{kTP[0], kRS[0], kRC[0]}; }
 
 }  // namespace trig
 }  // namespace mpc

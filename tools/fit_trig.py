@@ -95,11 +95,14 @@ if __name__ == "__main__" and "--small" in __import__("sys").argv:
     fit_small()
 
 
-def fit_tan_rational(xmax=1.1, m=3, n=4, iters=40, nodes=240):
+def fit_tan_rational(xmax=1.1, m=3, n=4, iters=40, nodes=240, monic=False):
     """Rational tan for the steering angle, no range reduction (|x| <= xmax):
         tan(x) = x + x^3 * P(x^2) / Q(x^2),   Q(0) = 1.
     Linearised least squares (Sanathanan-Koerner) with Lawson weights for a
-    near-minimax relative error of P/Q against T(s) = (tan(r) - r) / r^3."""
+    near-minimax relative error of P/Q against T(s) = (tan(r) - r) / r^3.
+    monic: P and Q divided by Q's leading coefficient before rounding (the
+    first Horner step of Q is then an add: no constant-bus move).
+    The shipped kTP/kTQ: --tan-rational --monic (m = n = 3)."""
     mp.mp.dps = 60
     smax = mp.mpf(xmax) ** 2
 
@@ -132,7 +135,16 @@ def fit_tan_rational(xmax=1.1, m=3, n=4, iters=40, nodes=240):
         if it >= 5:
             tot = sum(wi * abs(e) for wi, e in zip(w, err))
             w = [wi * abs(e) / tot * nodes for wi, e in zip(w, err)]
-    worst = max(abs((R(s) - T(s)) / T(s)) for s in (smax * k / 2000 for k in range(2001)))
+    if monic:
+        p = [c / q[-1] for c in p]
+        q = [c / q[-1] for c in q]
+    pd = [mp.mpf(d(c)) for c in p]
+    qd = [mp.mpf(d(c)) for c in q]
+
+    def Rd(s):
+        return mp.polyval(pd[::-1], s) / mp.polyval(qd[::-1], s)
+
+    worst = max(abs((Rd(s) - T(s)) / T(s)) for s in (smax * k / 2000 for k in range(2001)))
     print(f"// tan(x) = x + x^3 * TP(x^2) / TQ(x^2) on |x| <= {xmax}, rel. error of P/Q "
           f"{mp.nstr(worst, 5)}")
     print(f"constexpr double kTP[{m + 1}] = {{" + ", ".join(d(c).hex() for c in p[::-1]) + "};")
@@ -140,7 +152,10 @@ def fit_tan_rational(xmax=1.1, m=3, n=4, iters=40, nodes=240):
 
 
 if __name__ == "__main__" and "--tan-rational" in __import__("sys").argv:
-    fit_tan_rational()
+    if "--monic" in __import__("sys").argv:
+        fit_tan_rational(m=3, n=3, monic=True)
+    else:
+        fit_tan_rational()
 
 
 def two_over_pi_words(n=38):
