@@ -152,11 +152,12 @@ MPC_HD inline double ktan(double x, double y, bool odd) {
 // (tools/fit_trig.py --tan-rational --monic: degrees 3/3, rel. error of P/Q
 // 6.2e-17 with the rounded coefficients).  TQ is monic, so its first Horner
 // step is an add (no constant-bus move for a second coefficient operand).
-// One reciprocal estimate and one Newton step form 1/Q (rounded to nearest:
-// tools/micro/rcp_acc.hip finds no difference from 1/q over 2^30 mantissas,
-// so the host build's 1.0 / q gives the same bits); P * (1/Q) is not
-// corrected further: its rounding enters tan with weight x^3 R / tan <= 0.44.
-// ~14 VALU instead of the ~50 of a Cody-Waite reduction and the
+// One reciprocal estimate, one Newton step and one correction of the quotient
+// form P/Q.  The estimate is good to 2^-24.4 and one Newton step leaves 1/q
+// off its rounded value for ~40% of mantissas (tools/micro/rcp_acc.hip over
+// 2^30 of them), so the correction is what makes the device's quotient the
+// host build's (1.0 / q) bit for bit (tests/test_replica.py).
+// ~16 VALU instead of the ~50 of a Cody-Waite reduction and the
 // quadrant/cotangent reconstruction of tan_core.  The steering bound of the
 // reference's config is 60 deg = 1.047 rad; a larger |beta| makes the
 // candidate irregular (recomputed with tan_fast).
@@ -181,11 +182,13 @@ MPC_HD inline double tan_small(double x, const Leads* ld = nullptr) {
   q = fma_k(q, s, kTQ[3]);
 #if defined(__HIP_DEVICE_COMPILE__)
   double r = __builtin_amdgcn_rcp(q);
-  r = fma(r, fma(-q, r, 1.0), r);
 #else
-  const double r = 1.0 / q;
+  double r = 1.0 / q;
 #endif
-  return fma(x * s, p * r, x);
+  r = fma(r, fma(-q, r, 1.0), r);
+  double R = p * r;
+  R = fma(r, fma(-q, R, p), R);           // quotient correction
+  return fma(x * s, R, x);
 }
 
 // Core forms: valid for |x| <= kFastMax only (the caller guarantees it or
