@@ -318,6 +318,41 @@ __device__ __forceinline__ void wave_argmin(uint64_t& k, int64_t& i) {
   i = static_cast<int64_t>(lane63(static_cast<uint64_t>(i)));
 }
 
+// Minimum of a 32-bit value over the 64 lanes of a wave (all lanes active),
+// returned in every lane: the DPP pattern of wave_argmin with v_min_u32
+// (lanes a pattern does not feed get the identity 0xffffffff).
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+  auto lvl = [](uint32_t v, auto ctrl, auto rm) {
+    constexpr int C = decltype(ctrl)::value, M = decltype(rm)::value;
+    const uint32_t o = static_cast<uint32_t>(
+        __builtin_amdgcn_update_dpp(-1, static_cast<int>(v), C, M, 0xf, false));
+    return v < o ? v : o;
+  };
+  using std::integral_constant;
+  x = lvl(x, integral_constant<int, 0xB1>{}, integral_constant<int, 0xf>{});
+  x = lvl(x, integral_constant<int, 0x4E>{}, integral_constant<int, 0xf>{});
+  x = lvl(x, integral_constant<int, 0x141>{}, integral_constant<int, 0xf>{});
+  x = lvl(x, integral_constant<int, 0x140>{}, integral_constant<int, 0xf>{});
+  x = lvl(x, integral_constant<int, 0x142>{}, integral_constant<int, 0xA>{});
+  x = lvl(x, integral_constant<int, 0x143>{}, integral_constant<int, 0xC>{});
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 63));
+}
+
+// wave_argmin for 31-bit indices (a lane without a candidate holds the
+// sentinel (~0, INT64_MAX)): three 32-bit minima — the key's high word, its
+// low word among the lanes holding that high word, the index among the lanes
+// holding the whole key — give the same lexicographic minimum with ~40 VALU
+// instead of ~70 (two 64-bit compares and four selects per level).
+__device__ __forceinline__ void wave_argmin32(uint64_t& k, int64_t& i) {
+  const uint32_t hi = static_cast<uint32_t>(k >> 32), lo = static_cast<uint32_t>(k);
+  const uint32_t ix = k == ~0ull ? 0xffffffffu : static_cast<uint32_t>(i);
+  const uint32_t m1 = wave_min_u32(hi);
+  const uint32_t m2 = wave_min_u32(hi == m1 ? lo : 0xffffffffu);
+  const uint32_t m3 = wave_min_u32(hi == m1 && lo == m2 ? ix : 0xffffffffu);
+  k = (static_cast<uint64_t>(m1) << 32) | m2;
+  i = k == ~0ull ? INT64_MAX : static_cast<int64_t>(m3);
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

@@ -928,7 +928,7 @@ __global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
       }
     }
   }
-  block_argmin(best_k, best_i);
+  block_argmin<true>(best_k, best_i);   // (indices < n_cand < 2^31)
   if (threadIdx.x == 0) {
     if constexpr (MODE == kChainXchg)
       store_tagged_rec(&part[blockIdx.x - 1], best_k, best_i, epoch);

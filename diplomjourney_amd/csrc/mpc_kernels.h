@@ -44,10 +44,15 @@ struct Rec {
 
 // Block-level arg-min: wave shuffle, then the kWaves wave records via LDS.
 // The block winner ends up in thread 0.
+// IDX31: every index is below 2^31 (wave_argmin32).
+template <bool IDX31 = false>
 __device__ __forceinline__ void block_argmin(uint64_t& k, int64_t& i) {
   __shared__ uint64_t s_key[kWaves];
   __shared__ int64_t s_idx[kWaves];
-  wave_argmin(k, i);
+  if constexpr (IDX31)
+    wave_argmin32(k, i);
+  else
+    wave_argmin(k, i);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) {
     s_key[wave] = k;
@@ -423,7 +428,7 @@ __device__ __forceinline__ void rollout_argmin_body(
       }
     }
   }
-  block_argmin(best_k, best_i);
+  block_argmin<CPL == kCplWide>(best_k, best_i);   // (wide path: rows < 2^28 candidates)
   if (threadIdx.x == 0) part[blockIdx.x] = Rec{best_k, best_i};
 }
 
