@@ -719,8 +719,9 @@ def _episode_log(ep):
             for r in ep.read_log()]
 
 
-@pytest.mark.parametrize("wheelbase", [0.5, 0.45])
-def test_chained_episode_matches_separate_launches(engine, wheelbase):
+@pytest.mark.parametrize("wheelbase,n,ns", [(0.5, 50_000, 10), (0.45, 50_000, 10),
+                                            (0.5, 100_000, 3), (0.45, 100_000, 3)])
+def test_chained_episode_matches_separate_launches(engine, wheelbase, n, ns):
     """Chained steps (mpc_episode_chain_step: step k's rollout and step k-1's
     finalize + episode update in ONE launch, the tile blocks waiting on device
     for block 0's published constants) log exactly the steps of the
@@ -728,11 +729,12 @@ def test_chained_episode_matches_separate_launches(engine, wheelbase):
     events at p = 60/90/110 included — eagerly and replayed from a HIP graph
     whose last launch is the flush; a launch whose last tile is partial
     (50_000 = 97 tiles of 512 + 336).  Both wheelbase forms of the chained
-    kernel: L = 0.5 (a power of two, PL2) and L = 0.45 (v / L divided)."""
+    kernel: L = 0.5 (a power of two, PL2) and L = 0.45 (v / L divided);
+    N = 10 at 5e4 candidates and config B's shape (N = 3, 1e5)."""
     from diplomjourney_amd import math_model_tree as mmt
     from diplomjourney_amd.episode import DeviceEpisode
     integ = "rect+cum"
-    n, ns, steps = 50_000, 10, 130
+    steps = 130
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
     pool = [engine.sample_controls(V, B, n, ns, 500 + i) for i in range(8)]
@@ -779,13 +781,14 @@ def test_chained_episode_multi_tile_blocks(engine):
     assert ch.chain_error() == 0
 
 
-def test_chained_wheelbase_mismatch_is_flagged(engine):
+@pytest.mark.parametrize("ns", [10, 3])
+def test_chained_wheelbase_mismatch_is_flagged(engine, ns):
     """A chained launch whose cfg wheelbase form (power of two or not)
     differs from the state's constants sets chain error 2 instead of
     returning wrong costs silently."""
     from diplomjourney_amd import math_model_tree as mmt
     from diplomjourney_amd.episode import DeviceEpisode
-    n, ns = 20_000, 10
+    n = 20_000
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
     pool = [engine.sample_controls(V, B, n, ns, 40 + i) for i in range(2)]
