@@ -713,16 +713,16 @@ def kernel_pass(ep, pool, reps=100, warm=200):
 
 
 TRAFFIC_JSON = {"k_rollout_argmin_stream": "r03_traffic_stream.json",
-                "k_episode_chain": "r03_traffic_chain.json"}
+                "k_episode_chain": "r03_close/traffic_chain.json"}
 
 # fp64 VALU counters (tools/pmc_valu.sh: SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F64,
 # SQ_INSTS_VALU) of each kernel at the size it was measured on:
 # (kernel, integrator) -> (summary, candidates, horizon) — config C, or the
 # S1 = 451 full tree of config F (candidates = leaves)
-VALU_JSON = {("k_episode_chain", "rect+cum"): ("r03_valu_chain.json", 1_000_000, 10),
-             ("k_rollout_argmin_stream", "qk21"): ("r03_valu_qk21.json", 1_000_000, 10),
-             ("k_rollout_generated", "rect+cum"): ("r03_valu_gen.json", 1_000_000, 10),
-             ("k_ft_leaves", "rect+rot"): ("r03_valu_ft.json", 451 ** 3, 3)}
+VALU_JSON = {("k_episode_chain", "rect+cum"): ("r03_close/valu/chain.json", 1_000_000, 10),
+             ("k_rollout_argmin_stream", "qk21"): ("r03_close/valu/qk21.json", 1_000_000, 10),
+             ("k_rollout_generated", "rect+cum"): ("r03_close/valu/gen.json", 1_000_000, 10),
+             ("k_ft_leaves", "rect+rot"): ("r03_close/valu/ft.json", 451 ** 3, 3)}
 
 
 def valu_roofline(kernel, integrator, ms, n_cand, n_steps, note=None):
