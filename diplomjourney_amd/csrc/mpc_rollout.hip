@@ -346,6 +346,19 @@ int mpc_stream_probe(const double* v_sc, const double* beta_sc, int64_t n_cand,
   return last_hip_status();
 }
 
+__global__ void k_rcp_estimate(const double* __restrict__ q, double* __restrict__ r, int64_t n) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) r[i] = trig::rcp_estimate(q[i]);
+}
+
+int mpc_rcp_estimate(const double* q, double* r, int64_t n, mpc_stream_t stream) {
+  if (n < 0 || (n > 0 && (!q || !r))) return MPC_ERR_ARG;
+  if (n == 0) return MPC_OK;
+  k_rcp_estimate<<<static_cast<unsigned>(cdiv(n, kBlock)), kBlock, 0,
+                   reinterpret_cast<hipStream_t>(stream)>>>(q, r, n);
+  return last_hip_status();
+}
+
 int mpc_select_winner(const mpc_result_t* results, int32_t n, double incumbent,
                       mpc_result_t* out, mpc_stream_t stream) {
   if (!results || !out || n < 1) return MPC_ERR_ARG;

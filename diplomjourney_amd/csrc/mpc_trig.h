@@ -152,12 +152,16 @@ MPC_HD inline double ktan(double x, double y, bool odd) {
 // (tools/fit_trig.py --tan-rational --monic: degrees 3/3, rel. error of P/Q
 // 6.2e-17 with the rounded coefficients).  TQ is monic, so its first Horner
 // step is an add (no constant-bus move for a second coefficient operand).
-// One reciprocal estimate, one Newton step and one correction of the quotient
-// form P/Q.  The estimate is good to 2^-24.4 and one Newton step leaves 1/q
-// off its rounded value for ~40% of mantissas (tools/micro/rcp_acc.hip over
-// 2^30 of them), so the correction is what makes the device's quotient the
-// host build's (1.0 / q) bit for bit (tests/test_replica.py).
-// ~16 VALU instead of the ~50 of a Cody-Waite reduction and the
+// One reciprocal estimate and one Newton step form 1/Q; P * (1/Q) is not
+// corrected further (its rounding enters tan with weight x^3 R / tan <= 0.44).
+// The estimate (v_rcp_f64) is good to 2^-24.4 and one Newton step leaves the
+// reciprocal off its rounded value on ~40 % of mantissas
+// (tools/micro/rcp_acc.hip), so the host build reproduces the device bits only
+// with the device's own estimates: rcp_estimate() reads them from a table a
+// test installs (g_host_rcp_estimate, tests/replica_harness.cpp; the estimates
+// come from the device through mpc_rcp_estimate).  Without a table the host
+// build uses 1.0 / q (the CPU-side tests compare it within tolerances).
+// ~14 VALU instead of the ~50 of a Cody-Waite reduction and the
 // quadrant/cotangent reconstruction of tan_core.  The steering bound of the
 // reference's config is 60 deg = 1.047 rad; a larger |beta| makes the
 // candidate irregular (recomputed with tan_fast).
@@ -167,6 +171,19 @@ constexpr double kTP[4] = {0x1.2806dd56192d1p-14, -0x1.e9a6933b8c31cp-1, 0x1.4e6
 constexpr double kTQ[4] = {0x1.0000000000000p+0, -0x1.7f12a2265b864p+6, 0x1.c462cc7b84963p+10,
                            -0x1.e71b279e81d3cp+11};   // Q in [-3893, -1530] on |x| <= 1.1
 
+#if !defined(__HIP_DEVICE_COMPILE__)
+inline double (*g_host_rcp_estimate)(double) = nullptr;
+#endif
+
+// The hardware reciprocal estimate (device), or its host stand-in.
+MPC_HD inline double rcp_estimate(double q) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rcp(q);
+#else
+  return g_host_rcp_estimate ? g_host_rcp_estimate(q) : 1.0 / q;
+#endif
+}
+
 // Leading polynomial coefficients of the hot loop's trig, held in VGPRs by
 // the rollout kernel (one copy per lane instead of a v_mov per use); equal to
 // the constants, so results are bitwise those of the default arguments.
@@ -174,21 +191,20 @@ struct Leads {
   double tp, rs, rc;
 };
 
+// tan_small's denominator Q(s), s = x^2 (monic: the first step is an add).
+MPC_HD inline double tan_small_q(double s) {
+  double q = s + kTQ[1];
+  q = fma_k(q, s, kTQ[2]);
+  return fma_k(q, s, kTQ[3]);
+}
+
 MPC_HD inline double tan_small(double x, const Leads* ld = nullptr) {
   const double s = x * x;
   const double p = ld ? horner(kTP, s, 0, ld->tp, true) : horner(kTP, s);
-  double q = s + kTQ[1];
-  q = fma_k(q, s, kTQ[2]);
-  q = fma_k(q, s, kTQ[3]);
-#if defined(__HIP_DEVICE_COMPILE__)
-  double r = __builtin_amdgcn_rcp(q);
-#else
-  double r = 1.0 / q;
-#endif
+  const double q = tan_small_q(s);
+  double r = rcp_estimate(q);
   r = fma(r, fma(-q, r, 1.0), r);
-  double R = p * r;
-  R = fma(r, fma(-q, R, p), R);           // quotient correction
-  return fma(x * s, R, x);
+  return fma(x * s, p * r, x);
 }
 
 // Core forms: valid for |x| <= kFastMax only (the caller guarantees it or

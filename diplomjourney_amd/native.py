@@ -28,7 +28,7 @@ EXPORTS = (
     "mpc_version", "mpc_strerror", "mpc_workspace_bytes", "mpc_rollout_argmin",
     "mpc_rollout_partials", "mpc_rollout_finalize",
     "mpc_batched_workspace_bytes", "mpc_rollout_argmin_batched", "mpc_select_winner",
-    "mpc_stream_probe",
+    "mpc_stream_probe", "mpc_rcp_estimate",
     "mpc_sample_controls", "mpc_episode_state_bytes", "mpc_episode_reset",
     "mpc_episode_expand", "mpc_episode_advance", "mpc_episode_sample", "mpc_episode_partials",
     "mpc_episode_finalize", "mpc_episode_rollout", "mpc_episode_step", "mpc_episode_chain_step",
@@ -125,6 +125,8 @@ def lib():
                                              ctypes.c_size_t, _P, _P]
     L.mpc_stream_probe.restype = ctypes.c_int
     L.mpc_stream_probe.argtypes = [_P, _P, _I64, _I32, _P, ctypes.c_size_t, _P]
+    L.mpc_rcp_estimate.restype = ctypes.c_int
+    L.mpc_rcp_estimate.argtypes = [_P, _P, _I64, _P]
     L.mpc_select_winner.restype = ctypes.c_int
     L.mpc_select_winner.argtypes = [_P, _I32, _D, _P, _P]
     L.mpc_sample_controls.restype = ctypes.c_int

@@ -160,6 +160,13 @@ int mpc_select_winner(const mpc_result_t* results, int32_t n, double incumbent,
 int mpc_stream_probe(const double* v_sc, const double* beta_sc, int64_t n_cand,
                      int32_t n_steps, void* sink, size_t sink_bytes, mpc_stream_t stream);
 
+/* Verification probe (not a reference operation): the hardware reciprocal
+ * estimate the rollout's steering tangent starts from (v_rcp_f64, before its
+ * Newton step), r[i] for q[i], device arrays of n doubles.  A host build of
+ * the kernel's arithmetic (tests/replica_harness.cpp) installs these values to
+ * reproduce the device's bits: the estimate is not an IEEE operation. */
+int mpc_rcp_estimate(const double* q, double* r, int64_t n, mpc_stream_t stream);
+
 /* Synthetic candidate generator.  Candidate with
  * global index g = index_base + c:
  *   if const_prefix && g < n_v*n_beta: constant sequence u = (v_grid[g / n_beta],

@@ -53,17 +53,49 @@ def replica_lib():
                                    "-x", "hip", "-I", os.path.join(REPO, "include")])
     L.replica_rollout.argtypes = [ctypes.POINTER(MpcProblem), _P, _P, ctypes.c_int64,
                                   ctypes.c_int32, ctypes.c_int32, _P, _P]
+    L.replica_set_rcp_table.argtypes = [_P, _P, ctypes.c_int64]
+    L.replica_rcp_misses.restype = ctypes.c_int64
+    L.replica_tan_q.argtypes = [_P, ctypes.c_int64, _P]
     return L
 
 
-def replica_rollout(problem, v_sc, b_sc, integ="rect"):
-    """Host replica of the kernel arithmetic -> (states [N,3,C], costs [C])."""
+def device_rcp(q):
+    """The GPU's reciprocal estimates of q (mpc_rcp_estimate)."""
+    import torch
+    from diplomjourney_amd import native
+    qd = torch.as_tensor(np.ascontiguousarray(q, dtype=np.float64), device="cuda")
+    rd = torch.empty_like(qd)
+    native.check(native.lib().mpc_rcp_estimate(qd.data_ptr(), rd.data_ptr(), qd.numel(), None),
+                 "mpc_rcp_estimate")
+    torch.cuda.synchronize()
+    return rd.cpu().numpy()
+
+
+def replica_rollout(problem, v_sc, b_sc, integ="rect", device_estimates=False):
+    """Host replica of the kernel arithmetic -> (states [N,3,C], costs [C]).
+    device_estimates: the steering tangent's reciprocal estimates come from
+    the GPU (every denominator of b_sc), so the result is the device's bit for
+    bit; otherwise the host's 1.0 / q (within tolerances of it)."""
     from diplomjourney_amd.abi import INTEGRATORS
     v_sc = np.ascontiguousarray(v_sc, dtype=np.float64)
     b_sc = np.ascontiguousarray(b_sc, dtype=np.float64)
     ns, n = v_sc.shape
     states, costs = np.empty((ns, 3, n)), np.empty(n)
-    replica_lib().replica_rollout(ctypes.byref(problem), v_sc.ctypes.data_as(_P),
-                                  b_sc.ctypes.data_as(_P), n, ns, INTEGRATORS[integ],
-                                  states.ctypes.data_as(_P), costs.ctypes.data_as(_P))
+    L = replica_lib()
+    if device_estimates:
+        beta = np.unique(b_sc)
+        q = np.empty_like(beta)
+        L.replica_tan_q(beta.ctypes.data_as(_P), len(beta), q.ctypes.data_as(_P))
+        q = np.unique(q)
+        r = device_rcp(q)
+        L.replica_set_rcp_table(q.ctypes.data_as(_P), r.ctypes.data_as(_P), len(q))
+    try:
+        L.replica_rollout(ctypes.byref(problem), v_sc.ctypes.data_as(_P),
+                          b_sc.ctypes.data_as(_P), n, ns, INTEGRATORS[integ],
+                          states.ctypes.data_as(_P), costs.ctypes.data_as(_P))
+        if device_estimates:
+            assert L.replica_rcp_misses() == 0, "a denominator without its device estimate"
+    finally:
+        if device_estimates:
+            L.replica_set_rcp_table(None, None, 0)
     return states, costs

@@ -6,7 +6,50 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <unordered_map>
+
 #include "../diplomjourney_amd/csrc/mpc_device.h"
+
+// The device's reciprocal estimates (v_rcp_f64 is not an IEEE operation):
+// a GPU test fetches them for every denominator the rollout will form
+// (replica_tan_q -> mpc_rcp_estimate) and installs them here; without a table
+// the host build uses 1.0 / q.
+static std::unordered_map<uint64_t, double> g_rcp;
+static int64_t g_rcp_misses = 0;
+
+static double rcp_from_table(double q) {
+  uint64_t k;
+  memcpy(&k, &q, 8);
+  const auto it = g_rcp.find(k);
+  if (it == g_rcp.end()) {
+    ++g_rcp_misses;
+    return 1.0 / q;
+  }
+  return it->second;
+}
+
+extern "C" void replica_set_rcp_table(const double* q, const double* r, int64_t n) {
+  g_rcp.clear();
+  g_rcp_misses = 0;
+  if (n <= 0) {
+    mpc::trig::g_host_rcp_estimate = nullptr;
+    return;
+  }
+  g_rcp.reserve(static_cast<size_t>(n));
+  for (int64_t i = 0; i < n; ++i) {
+    uint64_t k;
+    memcpy(&k, &q[i], 8);
+    g_rcp[k] = r[i];
+  }
+  mpc::trig::g_host_rcp_estimate = rcp_from_table;
+}
+
+extern "C" int64_t replica_rcp_misses(void) { return g_rcp_misses; }
+
+// The denominators tan_small forms for these steering angles.
+extern "C" void replica_tan_q(const double* beta, int64_t n, double* q) {
+  for (int64_t i = 0; i < n; ++i) q[i] = mpc::trig::tan_small_q(beta[i] * beta[i]);
+}
 
 extern "C" int replica_rollout(const mpc_problem_t* p, const double* v, const double* b,
                                int64_t n_cand, int32_t n_steps, int32_t integ, double* states,

@@ -468,7 +468,8 @@ def test_full_size_config_e_batched(engine, oracle):
     exact = 0
     for r in range(R):
         cols = slice(r * cand, (r + 1) * cand)
-        st, costs = replica_rollout(probs[r], vh[:, cols], bh[:, cols], "rect+rot")
+        st, costs = replica_rollout(probs[r], vh[:, cols], bh[:, cols], "rect+rot",
+                                    device_estimates=True)
         k = int(np.argmin(costs))
         g = got[r]
         if g.index != k:     # only a near-tie below the constants' ulp noise

@@ -6,7 +6,9 @@ against the oracle (CPU) and against the GPU (bitwise).
   routines vs glibc, and x*x vs glibc pow(x, 2) in the cost).
 * GPU: the kernel's states (CoordinateTree output) and its winner's cost are
   the replica's BIT FOR BIT — the device code does exactly the IEEE
-  operations it was written to do.
+  operations it was written to do.  The one non-IEEE instruction, the
+  steering tangent's reciprocal estimate (v_rcp_f64), is supplied to the
+  replica from the device (harness.replica_rollout(device_estimates=True)).
 """
 import sys
 
@@ -76,7 +78,7 @@ def test_gpu_bitwise_equals_replica(engine, n, ns, integ):
     from diplomjourney_amd.abi import make_problem
     v, b = _case(n, ns, 11)
     p = make_problem(-1.0, 0.5, -2.2, 2, 3, 0.25, -0.5, 0.5, 7.45, 7.5)
-    st, costs = replica_rollout(p, v, b, integ)
+    st, costs = replica_rollout(p, v, b, integ, device_estimates=True)
     vd = torch.as_tensor(v, device="cuda")
     bd = torch.as_tensor(b, device="cuda")
     states = torch.empty((ns, 3, n), dtype=torch.float64, device="cuda")
@@ -94,8 +96,8 @@ def test_gpu_bitwise_equals_replica(engine, n, ns, integ):
 @pytest.mark.gpu
 @pytest.mark.parametrize("integ", ["rect", "rect+rot"])
 def test_gpu_trig_bitwise_equals_host_build(engine, integ):
-    """The device build of mpc_trig.h (hardware reciprocal estimate in
-    tan_small, device rint/fma) against its host build, through the
+    """The device build of mpc_trig.h (device rint/fma; tan_small's hardware
+    reciprocal estimates handed to the host build) against its host build, through the
     production kernel: every state of 2e6 candidates with uniformly random
     steering angles over the whole regular range |beta| <= 1.1 (not just the
     reference grid's 41 values) and random speeds, from a random start
@@ -106,7 +108,7 @@ def test_gpu_trig_bitwise_equals_host_build(engine, integ):
     v = rng.uniform(0.0, 1.0, (ns, n))
     b = rng.uniform(-1.1, 1.1, (ns, n))
     p = make_problem(0.3, -0.7, rng.uniform(-3, 3), 2, 3, 0, 0, 0.5, 0.05, 0.1)
-    st, costs = replica_rollout(p, v, b, integ)
+    st, costs = replica_rollout(p, v, b, integ, device_estimates=True)
     states = torch.empty((ns, 3, n), dtype=torch.float64, device="cuda")
     engine.rollout_argmin(p, torch.as_tensor(v, device="cuda"), torch.as_tensor(b, device="cuda"),
                           incumbent=INC_MAX, integrator=integ, states=states)
@@ -150,7 +152,7 @@ def test_gpu_irregular_candidates_stream_kernel(engine, integ):
     v[3, hit[32:]] = rng.uniform(1e7, 1e12, 32)        # dphi and the heading become huge
     cases.append((v, b, None))
     for v, b, want_irregular in cases:
-        st, costs = replica_rollout(p, v, b, integ)
+        st, costs = replica_rollout(p, v, b, integ, device_estimates=True)
         k = int(np.argmin(costs))
         if want_irregular:
             assert np.abs(b[:, k]).max() > 1.1       # the case exercises an irregular winner
