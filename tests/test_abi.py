@@ -91,6 +91,10 @@ def test_argument_validation_without_gpu():
                                  None) == abi.MPC_ERR_ARG  # ld < n_cand
     assert L.mpc_rollout_argmin_batched(fake, None, 0, fake, fake, 10, 3, 0, fake, 1 << 20,
                                         fake, None) == abi.MPC_ERR_ARG
+    # the verification probe: nothing to do, a negative count, missing arrays
+    assert L.mpc_rcp_estimate(None, None, 0, None) == abi.MPC_OK
+    assert L.mpc_rcp_estimate(fake, fake, -1, None) == abi.MPC_ERR_ARG
+    assert L.mpc_rcp_estimate(None, fake, 4, None) == abi.MPC_ERR_ARG
 
 
 def test_no_cpu_fallback(monkeypatch, tmp_path):
