@@ -90,7 +90,11 @@ FT_FLOPS_PER_LEAF = {"rect+rot": 34, "rect": 34, "qk21+rot": 78, "qk21": 78}
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks, one per GPU; without a launcher (WORLD_SIZE unset) N > 1 "
+                         "starts the N rank processes itself; under a launcher it must "
+                         "equal WORLD_SIZE")
+    ap.add_argument("--print-ranks", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--steps", type=int, default=None,
                     help="timed steps (default 500 for the ~40 us expansion workloads, so the "
                          "fixed graph-launch + sync cost (~0.2 ms) is amortised; 50 for F/G)")
@@ -312,12 +316,78 @@ def bench_dropin(args, wl, eng, rank, world, cpu):
         print(json.dumps(out), flush=True)
 
 
+def spawn_ranks(args):
+    """`python bench.py --gpus N` (N > 1) without a launcher: this process
+    stays GPU-free (it never initialises HIP: device counting does not) and
+    starts N rank processes of this same script, one per GPU, with RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their
+    environment — what `torch.distributed.run --nproc-per-node N` would do.
+    Rank 0 prints the JSON line on the shared stdout.  If one rank fails the
+    others are stopped; returns the worst exit status."""
+    import signal
+    import socket
+    import subprocess
+    n = args.gpus
+    if args.dist_backend == "nccl":
+        import torch
+        have = torch.cuda.device_count()
+        if have and n > have:
+            print(f"bench: --gpus {n} needs {n} GPUs for RCCL ranks ({have} visible); "
+                  "--dist-backend gloo rehearses more ranks than GPUs", file=sys.stderr)
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    worst = 0
+    while any(p.poll() is None for p in procs):
+        if any(p.returncode not in (None, 0) for p in procs):
+            stop()
+            t0 = time.time()
+            while any(p.poll() is None for p in procs) and time.time() - t0 < 30:
+                time.sleep(0.2)
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            break
+        time.sleep(0.1)
+    for p in procs:
+        rc = p.wait()
+        rc = 128 - rc if rc < 0 else rc     # killed by a signal: the shell's 128 + sig
+        worst = max(worst, rc)
+    return worst
+
+
 def main():
     args = parse()
     wl = WORKLOADS[args.workload]
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+              f"(torch.distributed.run --nproc-per-node {args.gpus}) or run "
+              f"`python bench.py --gpus {args.gpus}` without a launcher", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.print_ranks:     # launcher self-test (tests/test_host_logic.py): no GPU work
+        print(json.dumps({"rank": rank, "local_rank": local_rank, "world": world,
+                          "master": [os.environ.get("MASTER_ADDR"),
+                                     os.environ.get("MASTER_PORT")]}), flush=True)
+        return
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = (cpu_baseline_fulltree(args.cpu_seconds) if args.workload in ("F", "G")
@@ -373,9 +443,12 @@ def main():
     pool = make_pool(eng, ep, n_steps, args.steps) if inputs == "resident" else None
     rollout_ms = None
     # the launch that carries the step: the chained kernel (rollout of step k +
-    # completion of step k-1) or the rollout kernel
+    # completion of step k-1; on G > 1 its exchange form, which also selects
+    # over the gathered candidates and collects this rank's) or the rollout kernel
     chained = not exchange and getattr(ep, "chain", False) and inputs == "resident"
-    kernel = "k_episode_chain" if chained else "k_rollout_argmin_stream"
+    xchg_chain = exchange and getattr(ep, "chain", False) and inputs == "resident"
+    kernel = ("k_episode_chain" if chained else XCHG_KERNEL if xchg_chain
+              else "k_rollout_argmin_stream")
     main_run = run_steps(args, ep, pool, use_graph, world, device)
     use_graph = main_run["graph"]
     kern_ms = main_run["kernel_in_step_ms"]
@@ -384,6 +457,8 @@ def main():
         # for comparison: the same controls through the rollout kernel alone
         # (the chained launch adds block 0's completion of the previous step)
         rollout_ms = kernel_pass(ep, pool)
+    elif xchg_chain:
+        kern_ms = exchange_chain_pass(ep, pool)
     elif inputs == "generated":
         pass   # events around the generated rollout + selection (no HBM roofline)
     elif hasattr(ep, "partials"):
@@ -419,8 +494,25 @@ def main():
     bytes_launch = 16.0 * n_steps * ep.n_local
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     value = n_total * args.steps / elapsed
+    # self-validation: a chained / exchange step whose bounded device wait
+    # timed out ran on speculated constants or dropped a rank's candidate —
+    # such a run reports no throughput (max over ranks; exit status 3)
+    chain_err, log = 0, None
     if not args.host_loop:
-        log = ep.read_log()
+        from diplomjourney_amd.episode import ChainError
+        try:
+            log = ep.read_log()
+        except ChainError as e:
+            chain_err = e.code
+    chain_err = int(max_over_ranks(chain_err, device))
+    if chain_err:
+        from diplomjourney_amd.episode import CHAIN_ERRORS
+        print(f"bench: chain_error {chain_err} on some rank: "
+              f"{CHAIN_ERRORS.get(chain_err, 'unknown')}; no result", file=sys.stderr, flush=True)
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        sys.exit(3)
+    if not args.host_loop:
         if args.dump_log and rank == 0:
             with open(args.dump_log, "w") as fh:
                 json.dump([{f: getattr(r, f) for f, _ in r._fields_} for r in log], fh)
@@ -463,6 +555,7 @@ def main():
                           "controller receives the chosen control (math_model_tree.py:429); "
                           "reference: 0.361 s p50 per predictive_control at N=3, 451 "
                           "candidates (SURVEY §6)"),
+        "chain_error": chain_err,
         "kernel_ms": kern_ms, "kernel_in_step_ms": main_run["kernel_in_step_ms"],
         "roofline": (None if inputs == "generated" else
                      roofline(achieved, bytes_launch, args.traffic_json, kernel=kernel)),
@@ -712,8 +805,41 @@ def kernel_pass(ep, pool, reps=100, warm=200):
     return k0.elapsed_time(k1) / reps
 
 
+def max_over_ranks(x, device):
+    """max of a number over the ranks (x itself without a process group)."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return x
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def exchange_chain_pass(ep, pool, reps=100, warm=200):
+    """The exchange-form chained launch (mpc_episode_exchange_step: selection
+    over step k-1's gathered candidates + episode update + rollout of step k +
+    this rank's candidate) alone: per launch a pair of HIP events on the
+    episode's stream around the launch only — the all_gather that follows it
+    is outside the pair — averaged over REPS real steps after WARM untimed
+    ones (the clock ramp, as chain_pass)."""
+    import torch
+    for i in range(warm):
+        ep.step(controls=pool[i % len(pool)])
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(reps)]
+    for i in range(reps):
+        ep.step(events=evs[i], controls=pool[(i + 1) % len(pool)])
+    ep.flush()
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in evs) / reps
+
+
+# the exchange form of the chained kernel (k_episode_chain<..., kChainXchg, ...>)
+XCHG_KERNEL = "k_episode_chain[exchange]"
 TRAFFIC_JSON = {"k_rollout_argmin_stream": "r03_traffic_stream.json",
-                "k_episode_chain": "r03_close/traffic_chain.json"}
+                "k_episode_chain": "r03_close/traffic_chain.json",
+                XCHG_KERNEL: "r04/traffic_chain_xchg.json"}
 
 # fp64 VALU counters (tools/pmc_valu.sh: SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F64,
 # SQ_INSTS_VALU) of each kernel at the size it was measured on:

@@ -581,18 +581,44 @@ __global__ __launch_bounds__(kFinBlock) void k_episode_advance_cand(
   advance_from_candidates<INTEG, ROT>(c, S, g, n, out, log, cap, 0u, &lds);
 }
 
-// A tile block's record in an exchange step: ONE 16-B `sc1` store {cost key,
-// (epoch << 32) | local index} — a data-tagged granule that block 0 of the
-// same launch polls for (no counter, no wait in the tile block).  No
-// candidate: index 0xffffffff.
+// A tile block's record in an exchange step: ONE 16-B `sc1` store that block
+// 0 of the same launch polls for (no counter, no wait in the tile block).
+// Freshness must not rest on the 16-B store and load being single-copy
+// atomic (the memory model promises that only up to 8 B), so EACH 8-B half
+// carries the launch's 16-bit tag in its low bits and block 0 accepts the
+// record only when both halves show it:
+//   word 0 = key[63:16] << 16 | tag
+//   word 1 = key[15:0] << 48 | index[31:0] << 16 | tag
+// (the 64-bit cost key and a 32-bit local index; no candidate: index
+// 0xffffffff).  A half torn from an older record carries another tag (or the
+// 0 of a consumed record) and is polled again.
+__device__ __forceinline__ uint32_t rec_tag(uint32_t epoch) {
+  return epoch % 0xffffu + 1u;   // in [1, 0xffff]; consecutive epochs differ, 0 = untagged
+}
+
 __device__ __forceinline__ void store_tagged_rec(Rec* dst, uint64_t key, int64_t idx,
                                                  uint32_t epoch) {
-  const uint64_t lo = idx == INT64_MAX ? 0xffffffffull
+  const uint64_t ix = idx == INT64_MAX ? 0xffffffffull
                                        : static_cast<uint64_t>(static_cast<uint32_t>(idx));
+  const uint64_t tag = rec_tag(epoch);
+  const uint64_t w0 = (key & ~0xffffull) | tag;
+  const uint64_t w1 = (key << 48) | (ix << 16) | tag;
   asm volatile("global_store_dwordx4 %0, %1, off sc1"
                :
-               : "v"(dst), "v"(u64x2{key, (static_cast<uint64_t>(epoch) << 32) | lo})
+               : "v"(dst), "v"(u64x2{w0, w1})
                : "memory");
+}
+
+__device__ __forceinline__ bool tagged_rec_fresh(const u64x2& r, uint32_t tag) {
+  return static_cast<uint32_t>(r.x & 0xffffu) == tag && static_cast<uint32_t>(r.y & 0xffffu) == tag;
+}
+
+__device__ __forceinline__ uint64_t tagged_rec_key(const u64x2& r) {
+  return (r.x & ~0xffffull) | (r.y >> 48);
+}
+
+__device__ __forceinline__ uint32_t tagged_rec_index(const u64x2& r) {
+  return static_cast<uint32_t>(r.y >> 16);
 }
 
 // Block 0 of an exchange step, after publishing: wait until every tile
@@ -613,13 +639,13 @@ __device__ void collect_local_candidate(const Rec* __restrict__ part, int n_part
     ptr[q] = part + (p < n_part ? p : n_part - 1);
   }
   bool timed_out = false;
+  const uint32_t tag = rec_tag(epoch);
   for (uint32_t it = 0;; ++it) {
     load8_rec_sc1(ptr, r);
     bool ok = true;
 #pragma unroll
     for (int q = 0; q < 8; ++q)
-      if (threadIdx.x + q * kBlock < n_part)
-        ok = ok && static_cast<uint32_t>(r[q].y >> 32) == epoch;
+      if (threadIdx.x + q * kBlock < n_part) ok = ok && tagged_rec_fresh(r[q], tag);
     if (__syncthreads_and(ok)) break;
     if (it >= kChainSpinLimit) {   // uniform: every thread counts the same passes
       timed_out = true;
@@ -632,17 +658,18 @@ __device__ void collect_local_candidate(const Rec* __restrict__ part, int n_part
   if (!timed_out) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const uint32_t lo = static_cast<uint32_t>(r[q].y);
+      const uint32_t lo = tagged_rec_index(r[q]);
       const int64_t idx = lo == 0xffffffffu ? INT64_MAX : static_cast<int64_t>(lo);
+      const uint64_t key = tagged_rec_key(r[q]);
       if (threadIdx.x + q * kBlock < n_part) {
-        if (rec_less(r[q].x, idx, k, i)) {
-          k = r[q].x;
+        if (rec_less(key, idx, k, i)) {
+          k = key;
           i = idx;
         }
-        // consumed: untag it.  A replayed HIP graph repeats its launches'
-        // epochs, so a record left tagged would pass for the replay's own
-        // before that launch's tile block stores it.
-        const_cast<Rec*>(ptr[q])->idx = 0;
+        // consumed: untag both halves.  A replayed HIP graph repeats its
+        // launches' epochs, so a record left tagged would pass for the
+        // replay's own before that launch's tile block stores it.
+        *const_cast<u64x2*>(reinterpret_cast<const u64x2*>(ptr[q])) = u64x2{0ull, 0ull};
       }
     }
   } else if (threadIdx.x == 0) {

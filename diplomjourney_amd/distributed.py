@@ -5,12 +5,21 @@ Rank g owns the contiguous candidate range [g*C/G, (g+1)*C/G); its kernel
 reports global indices (index_base), so the lowest-index tie-break is the same
 as on one device and in the reference's ascending scan.
 
-RCCL has no (min, index) reduction, so the exchange is ONE all_gather of the
-per-rank 808-byte result records (cost, global index, found, winner
-trajectory) followed by the lexicographic (cost, index) selection on every
-rank — semantically the all-reduce(min+index) of the north star, and it
-carries the winner's trajectory in the same collective, so no second
-broadcast is needed.  The payload is G x 808 B: pure latency over xGMI.
+RCCL has no (min, index) reduction, so every exchange is ONE all_gather
+followed by the lexicographic (cost, global index) selection on every rank —
+semantically the north star's all-reduce(min+index):
+  * the device-resident chained step (DeviceEpisode(exchange=True,
+    chain=True), the bench's N > 1 path): `gather_bytes` of each rank's
+    536-byte mpc_candidate_t (cost, global index, the candidate's N
+    controls); the NEXT launch's block 0 selects the winner and re-rolls it
+    from the gathered controls (mpc_episode.h advance_from_candidates);
+  * the generic per-call path (Episode, the drop-in's shards):
+    `exchange_winner` = all_gather of the 808-byte mpc_result_t records
+    (winner trajectory included) + k_select_winner.
+Either payload is G x (536 | 808) B: pure latency over xGMI.  RCCL with more
+than one rank has not yet run on hardware in this repo's tests (1-rank RCCL
+groups, gloo ranks sharing a GPU, and an RCCL clique of one GPU from the C
+host are what the tests exercise).
 """
 import math
 

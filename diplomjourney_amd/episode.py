@@ -31,6 +31,23 @@ from .abi import (CANDIDATE_BYTES, LOG_BYTES, MPC_EP_ARRIVED, MPC_EP_BREAK, MPC_
 from .distributed import exchange_winner, gather_bytes, gather_results, shard_range
 from . import native
 
+CHAIN_ERRORS = {
+    1: "a chained launch's tile blocks timed out waiting for block 0's published constants "
+       "(the step was scored on speculated constants)",
+    2: "the state was reset with another wheelbase form (power of two or not) than the "
+       "launch's cfg",
+    3: "an exchange launch's block 0 timed out collecting its tile records (this rank's "
+       "candidate dropped out of the global arg-min)",
+}
+
+
+class ChainError(RuntimeError):
+    """A device-resident episode's bounded wait failed (EpisodeState::chain_error)."""
+
+    def __init__(self, code):
+        self.code = int(code)
+        super().__init__(f"chain_error {self.code}: {CHAIN_ERRORS.get(self.code, 'unknown')}")
+
 
 class Episode:
     def __init__(self, engine, n_cand_total, n_steps, rank=0, world=1, seed=20261015,
@@ -219,7 +236,13 @@ class DeviceEpisode:
     """The same episode with its state in HBM (mpc_episode_* C ABI): a step
     is enqueued without any host synchronisation, so the host only launches
     and the GPU runs steps back to back.  `read_log()` syncs and decodes the
-    per-step records."""
+    per-step records (and raises ChainError if a device wait timed out).
+
+    Capturing chained / exchange steps into a hipGraph: end the captured
+    sequence with `flush()` inside the capture.  A replay repeats the captured
+    launches' epochs; the flush's update clears the published constants' tags,
+    without it the next replay's launch with the last epoch could accept the
+    previous replay's constants (include/mpc_rollout.h)."""
 
     def __init__(self, engine, n_cand_total, n_steps, rank=0, world=1, seed=20261015,
                  integrator="rect", group=None, start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3),
@@ -246,7 +269,9 @@ class DeviceEpisode:
         self.winner = torch.zeros(RESULT_BYTES, dtype=torch.uint8, device=dev)
         self.log_capacity = int(log_capacity)
         self.log = torch.zeros(self.log_capacity * LOG_BYTES, dtype=torch.uint8, device=dev)
-        self.ws = torch.empty(self.lib.mpc_workspace_bytes(self.n_local, self.n_steps),
+        # zeroed: an exchange step's tagged block records must never find an
+        # old allocation's bytes carrying a tag (mpc_episode.h store_tagged_rec)
+        self.ws = torch.zeros(self.lib.mpc_workspace_bytes(self.n_local, self.n_steps),
                               dtype=torch.uint8, device=dev)
         from .abi import INTEGRATORS
         self._integ = INTEGRATORS[integrator]
@@ -262,7 +287,7 @@ class DeviceEpisode:
         # (mpc_episode_chain_step; caller-resident controls, aligned path);
         # flush() completes the last one.
         self.chain = bool(chain)
-        self._ws = [self.ws, torch.empty_like(self.ws)] if self.chain else [self.ws]
+        self._ws = [self.ws, torch.zeros_like(self.ws)] if self.chain else [self.ws]
         # exchange + chain: this rank's best candidate of the step (the
         # all_gather payload of mpc_episode_exchange_step)
         self.cand = torch.zeros(CANDIDATE_BYTES, dtype=torch.uint8, device=dev)
@@ -335,6 +360,9 @@ class DeviceEpisode:
                 self.world if pend is not None else 0, self.winner.data_ptr(),
                 self.cand.data_ptr(), self.log.data_ptr(), self.log_capacity, st),
                 "mpc_episode_exchange_step")
+            if events:                   # the launch alone, not the collective after it
+                events[1].record()
+                events = None
             self._pending = gather_bytes(self.cand, self.group)
         if events:
             events[1].record()
@@ -466,8 +494,16 @@ class DeviceEpisode:
                 and v.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
 
     def read_log(self):
+        """Complete any pending step, sync, and decode the per-step records.
+        Raises ChainError if a chained / exchange step's bounded device wait
+        timed out (mpc_episode_chain_error != 0): such a step ran on
+        speculated constants or dropped this rank's candidate, so its log
+        records must not be trusted."""
         self.flush()
         torch.cuda.current_stream().synchronize()
+        err = self.chain_error()
+        if err:
+            raise ChainError(err)
         raw = self.log.cpu().numpy().tobytes()
         n = min(self.steps_enqueued, self.log_capacity)
         recs = [MpcEpisodeLog.from_buffer_copy(raw[i * LOG_BYTES:(i + 1) * LOG_BYTES])

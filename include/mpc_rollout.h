@@ -16,6 +16,13 @@
  * Data layout in HBM (SoA, step-major, fp64):
  *   v_sc[s * n_cand + c], beta_sc[s * n_cand + c]   s < n_steps, c < n_cand
  * Candidate c's global index is index_base + c (contiguous shards across GPUs).
+ *
+ * The fast ("aligned") path: n_cand even, v_sc and beta_sc 16-B aligned, and
+ * rows of fewer than 2^28 candidates (the LDS-DMA control loads address a row
+ * as an SGPR base plus a 32-bit lane byte offset).  Other shapes run the one-
+ * candidate-per-lane kernel (same results, several times slower) in the
+ * one-shot and two-launch entries; the chained and exchange entries, which
+ * exist only on the aligned path, return MPC_ERR_UNSUPPORTED.
  */
 #ifndef DIPLOMJOURNEY_AMD_MPC_ROLLOUT_H
 #define DIPLOMJOURNEY_AMD_MPC_ROLLOUT_H
@@ -295,7 +302,12 @@ int mpc_episode_step(void* state, const double* v_sc, const double* beta_sc, int
  * mpc_workspace_bytes(n_cand, n_steps) each, alternated.  cfg must be the
  * configuration the state was reset with: the launch picks its wheelbase form
  * (L a power of two or not) from cfg->L, the rollout uses the state's
- * constants; a mismatch sets chain error 2 (mpc_episode_chain_error). */
+ * constants; a mismatch sets chain error 2 (mpc_episode_chain_error).
+ * hipGraph capture: a captured sequence of chained (or exchange) steps must
+ * END with its completing call (mpc_episode_finalize / _exchange_flush), which
+ * clears the published constants' epoch tags — a replay repeats the captured
+ * epochs, so a sequence left open would let the next replay's launch with the
+ * last epoch take the previous replay's constants. */
 #define MPC_CHAIN_FINALIZE 1
 int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t mode,
                            uint32_t epoch, const double* v_sc, const double* beta_sc,
@@ -313,13 +325,16 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
  *            re-rolled from its gathered controls into out_prev (the global
  *            winner, on every rank), the episode update, this step's
  *            constants published; then it collects this launch's block
- *            records (epoch-tagged 16-B granules, no counter) and writes this
- *            rank's best candidate (cost, global index, controls) to `local`;
+ *            records (16-B granules whose two 8-B halves each carry the
+ *            launch's tag: no counter, and no reliance on 16-B single-copy
+ *            atomicity) and writes this rank's best candidate (cost, global
+ *            index, controls) to `local`;
  *   other blocks: the rollout of this rank's shard (index_base).
  * ws: mpc_workspace_bytes(n_cand, n_steps) (one; consecutive launches are
  * stream-ordered).  The last step is completed by mpc_episode_exchange_flush
- * over its gathered candidates, which ends the chain.  A collection that
- * timed out sets chain error 3. */
+ * over its gathered candidates, which ends the chain (and must end a captured
+ * sequence, as above).  A collection that timed out sets chain error 3.
+ * n_cand < 2^31 (local indices travel in 32 bits of the tagged records). */
 int mpc_episode_exchange_step(const mpc_episode_config_t* cfg, void* state, uint32_t epoch,
                               const double* v_sc, const double* beta_sc, int64_t n_cand,
                               int32_t n_steps, int64_t index_base, int32_t integrator, void* ws,

@@ -162,6 +162,54 @@ def test_bench_defaults(monkeypatch):
     assert parse("--inputs", "generated").inputs == "generated"
 
 
+def _bench(args, env_extra=None, drop=("WORLD_SIZE", "RANK", "LOCAL_RANK")):
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in drop}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(repo, "bench.py"), *args], env=env,
+                          capture_output=True, text=True, timeout=120, cwd=repo)
+
+
+def test_bench_gpus_world_size_mismatch_fails():
+    """Under a launcher, --gpus must equal WORLD_SIZE: a mismatch exits 2
+    before any GPU or CPU-baseline work instead of running a mislabelled line."""
+    r = _bench(["--gpus", "4"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr, r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    r = _bench(["--gpus", "1"], {"WORLD_SIZE": "8", "RANK": "3", "LOCAL_RANK": "3"})
+    assert r.returncode == 2
+
+
+def test_bench_gpus_spawns_one_process_per_rank():
+    """`python bench.py --gpus N` without a launcher starts N rank processes
+    of itself with RANK / LOCAL_RANK / WORLD_SIZE and one shared
+    MASTER_ADDR 127.0.0.1:port (the launcher self-test prints each rank's view
+    instead of running GPU work)."""
+    import json
+    r = _bench(["--gpus", "3", "--dist-backend", "gloo", "--print-ranks"])
+    assert r.returncode == 0, r.stderr
+    ranks = sorted((json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")),
+                   key=lambda d: d["rank"])
+    assert [d["rank"] for d in ranks] == [0, 1, 2]
+    assert all(d["world"] == 3 and d["local_rank"] == d["rank"] for d in ranks)
+    assert len({tuple(d["master"]) for d in ranks}) == 1 and ranks[0]["master"][0] == "127.0.0.1"
+
+
+def test_bench_spawned_rank_failure_fails_the_run():
+    """A failing rank fails the spawned run with its status (here every rank
+    rejects an inconsistent launch), and no JSON line is printed."""
+    r = _bench(["--gpus", "2", "--dist-backend", "gloo", "--print-ranks"],
+               {"WORLD_SIZE": "2"}, drop=("RANK", "LOCAL_RANK"))
+    assert r.returncode == 0          # under a launcher: WORLD_SIZE matches, no spawn
+    r = _bench(["--gpus", "2", "--dist-backend", "gloo", "--workload", "C", "--steps", "4",
+                "--cpu-seconds", "0"], {"DIPLOMJOURNEY_MPC_LIB": "/nonexistent/lib.so"})
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
 def test_tree_grids_match_reference_enumeration():
     """run_math_model.run_tree_batched's vectorised grids: per robot exactly
     vector_of_velocities x vector_of_beta_angles (math_model_tree.py:239-256)

@@ -1,7 +1,11 @@
 """Summarise tools/pmc.sh counter passes for the rollout kernel into a JSON
 file bench.py reads for roofline.traffic (--traffic-json).
 
-    python tools/pmc_summary.py gpurun_out/<tag> out.json [algorithmic_bytes] [kernel]
+    python tools/pmc_summary.py gpurun_out/<tag> out.json [algorithmic_bytes] [kernel] [label]
+
+kernel: a substring of the rocprof kernel name (e.g. "k_episode_chain<1, 2, 3"
+for the exchange form); label: the name written to the summary's "kernel"
+field, the key bench.py matches (default: kernel).
 
 HBM bytes per launch = 2 x FETCH_SIZE (KB x 1024) + WRITE_SIZE: on gfx950
 FETCH_SIZE counts half the bytes of a 16-B-per-lane streaming read and
@@ -18,6 +22,7 @@ def main():
     root, out = sys.argv[1], sys.argv[2]
     algo = float(sys.argv[3]) if len(sys.argv) > 3 else 160e6   # 16 B x N x C of the runs
     kernel = sys.argv[4] if len(sys.argv) > 4 else "k_rollout_argmin_stream"
+    label = sys.argv[5] if len(sys.argv) > 5 else kernel
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     for f in sorted(glob.glob(os.path.join(root, "pmc*", "p_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
@@ -37,7 +42,8 @@ def main():
         f64 = 64.0 * (2 * med["SQ_INSTS_VALU_FMA_F64"] + med.get("SQ_INSTS_VALU_ADD_F64", 0)
                       + med.get("SQ_INSTS_VALU_MUL_F64", 0) + med.get("SQ_INSTS_VALU_TRANS_F64", 0))
     res = {
-        "kernel": kernel,
+        "kernel": label,
+        "kernel_name_filter": kernel,
         "fp64_ops_per_launch": f64,
         "hbm_bytes_per_launch": 2.0 * fetch_b + write_b,
         "algorithmic_bytes_per_launch": algo,

@@ -5,6 +5,8 @@ launches stream from HBM as in the bench).
     python tools/prof_kernel.py [n_cand] [n_steps] [integ] [reps] [batches]
 integ "chain": chained rect+cum episode steps instead (mpc_episode_chain_step,
 the bench default's launch: rollout of step k + completion of step k-1);
+"xchg": the exchange form of the chained step (mpc_episode_exchange_step +
+the RCCL all_gather, over a 1-rank nccl group: the N > 1 bench's launch);
 "generated": generated-controls episode steps (k_rollout_generated, rect+cum);
 "fulltree": config F's full-tree MPC steps (k_ft_leaves, S1 = 451, n_cand and
 n_steps ignored)."""
@@ -51,12 +53,25 @@ def main():
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
     pool = [eng.sample_controls(V, B, n, ns, 7 + i) for i in range(nb)]
-    if integ == "chain":
+    if integ in ("chain", "xchg"):
         from diplomjourney_amd.episode import DeviceEpisode
-        ep = DeviceEpisode(eng, n, ns, integrator="rect+cum", chain=True, log_capacity=8192)
+        xchg = integ == "xchg"
+        if xchg:
+            import socket
+            import torch.distributed as dist
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                port = s.getsockname()[1]
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                    world_size=1, device_id=torch.device("cuda", 0))
+        ep = DeviceEpisode(eng, n, ns, integrator="rect+cum", chain=True, exchange=xchg,
+                           log_capacity=8192)
         for i in range(reps):
             ep.step(controls=pool[i % nb])
         ep.flush()
+        if xchg:
+            torch.cuda.synchronize()
+            dist.destroy_process_group()
     else:
         prob = make_problem(0.0, 0.0, 0.3, 2, 3, 0, 0, 0.5, 0.05, 0.1)
         for i in range(reps):
