@@ -75,8 +75,8 @@ WORKLOADS = {
 WORKLOADS["R"] = dict(n_steps=3, per_gpu=None, robots=1000,
                       desc="run_math_model.py's 1000-episode loop (:231-280) over the tree "
                            "expansion of math_model_tree.py (acceleration-limited grid <= 451 "
-                           "candidates, N=3): one robot per episode, lockstep, one batched "
-                           "launch pair per MPC step (mpc_rollout_argmin_batched)")
+                           "candidates, N=3): one robot per episode, device-resident, one "
+                           "block per robot (mpc_episodes_run)")
 WORKLOADS["G"] = dict(n_steps=3, per_gpu=None, robots=1000,
                       desc="run_math_model.py's 1000 episodes (SURVEY 8f 4): one robot per "
                            "episode, lockstep, one batched full-tree launch per MPC step, "
@@ -1090,56 +1090,65 @@ def bench_fulltree(args, wl, eng, rank, world, cpu):
 def bench_tree_episodes(args, wl, eng, rank, world, cpu):
     """The named entry: run_math_model.py's seeded episode loop
     for 1000 episodes, its MPC step the tree expansion (Fact 2), robots
-    sharded over ranks (no exchange), lockstep on each rank: one batched
-    launch pair per MPC step of all running episodes.  A timed step = one
-    lockstep MPC step (grids on the host, [3, R x 451] candidates up, the
-    batched expansion, R result records down, the per-robot post-processing);
-    K = --steps caps an episode's calls."""
+    sharded over ranks (no exchange), device-resident (episode.DeviceEpisodes:
+    one block per robot runs its episode's MPC steps back to back — grid,
+    enumeration, expansion, winner, update — in ONE launch).  Timed: the
+    launch of up to K = --steps MPC steps of every episode (K caps an
+    episode's calls; the log of every step is written) between syncs;
+    ms_per_step = that time / the longest episode's calls (a lockstep-
+    equivalent step of all running episodes)."""
     import torch
     import torch.distributed as dist
     from diplomjourney_amd import run_math_model as rmm
+    from diplomjourney_amd.abi import MPC_EP_ARRIVED, MPC_EP_BREAK
     from diplomjourney_amd.distributed import shard_range
-    from diplomjourney_amd.episode import percentile
+    from diplomjourney_amd.episode import DeviceEpisodes, tree_episode_config
     starts = rmm.draw_starts(wl["robots"], seed=20261015)
     lo, hi = shard_range(len(starts), rank, world)
-    rmm.run_tree_batched(starts[lo:hi], max_calls=max(1, args.warmup), integrator=args.integrator,
-                         engine=eng)
+    cfgs = [tree_episode_config(s, args.steps) for s in starts[lo:hi]]
+    eps = DeviceEpisodes(eng, cfgs, 3, args.integrator, log_capacity=args.steps)
+    for _ in range(max(1, args.warmup)):                # warmup: whole runs
+        eps.reset()
+        eps.run(args.steps)
+    eps.reset()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    st = {}
-    outs = rmm.run_tree_batched(starts[lo:hi], max_calls=args.steps, integrator=args.integrator,
-                                engine=eng, stats=st)
+    eps.run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    calls = sum(len(r) for r, _ in outs)
-    lockstep = st["steps"]
-    cands = st["candidates"]      # each call's |V| x |B| (the padding is not counted)
-    t = torch.tensor([elapsed, calls, cands, lockstep], dtype=torch.float64, device=eng.device)
+    calls, stop, cands = eps.read_progress()
+    t = torch.tensor([elapsed, float(calls.sum()), float(cands.sum()), float(calls.max())],
+                     dtype=torch.float64, device=eng.device)
     if world > 1:
         mx = t[[0, 3]].clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        elapsed, lockstep = float(mx[0]), int(mx[1])
-        calls, cands = float(t[1]), float(t[2])
+        t[0], t[3] = mx[0], mx[1]
+    elapsed, n_calls, n_cands, lockstep = (float(t[0]), int(t[1]), int(t[2]), int(t[3]))
     stops = {}
-    for _, st in outs:
-        stops[st] = stops.get(st, 0) + 1
+    for st in stop:
+        k = ("recursive_error" if st & MPC_EP_BREAK else
+             "on_target" if st & MPC_EP_ARRIVED else "max_calls")
+        stops[k] = stops.get(k, 0) + 1
     out = {
-        "metric": METRIC, "value": cands / elapsed, "unit": "rollouts/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / lockstep * 1e3,
+        "metric": METRIC, "value": n_cands / elapsed, "unit": "rollouts/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / max(1, lockstep) * 1e3,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (the script's seeded start/target draws)",
         "config": {"workload": wl["desc"], "n_steps": 3, "episodes": wl["robots"],
-                   "mpc_calls": calls, "lockstep_steps": lockstep,
+                   "mpc_calls": n_calls, "lockstep_steps": lockstep,
                    "integrator": args.integrator, "episode_stops_rank0": stops,
+                   "episode_loop": "device-resident: one block per robot, one launch for all "
+                                   "steps (mpc_episodes_run)",
                    "parallelism": f"robot-sharded x{world}, no exchange"},
         "episodes_per_s": wl["robots"] / elapsed,
         "p50_ms": None,
-        "p50_note": "ms_per_step = one lockstep MPC step of every running episode",
+        "p50_note": "ms_per_step = the run's time / the longest episode's MPC calls",
         "roofline": None, "cpu_baseline": cpu,
     }
     if rank == 0:

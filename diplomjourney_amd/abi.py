@@ -79,7 +79,7 @@ class MpcEpisodeConfig(ctypes.Structure):
         "ratio_beta", "beta_bound", "radius_u_turn", "turn_distance", "event_target_x",
         "event_target_y", "incumbent0")] + [(n, ctypes.c_int32) for n in (
         "p_turn_right", "p_turn_left", "p_new_target", "slow_new_target", "slow_turn",
-        "max_steps", "enumerate", "reserved_")] + [("seed", ctypes.c_uint64)]
+        "max_steps", "enumerate", "stop_rule")] + [("seed", ctypes.c_uint64)]
 
 
 # mpc_episode_log_t.status bits (include/mpc_rollout.h)
@@ -93,6 +93,12 @@ class MpcEpisodeLog(ctypes.Structure):
                 ("episode", ctypes.c_int32), ("found", ctypes.c_int32),
                 ("status", ctypes.c_int32)] + [(n, ctypes.c_double) for n in (
                     "cost", "x", "y", "phi", "v", "beta")]
+
+
+class MpcEpisodesProgress(ctypes.Structure):
+    """mpc_episodes_progress_t: one robot of the batched device episodes."""
+    _fields_ = [("calls", ctypes.c_int32), ("stop", ctypes.c_int32),
+                ("candidates", ctypes.c_int64)]
 
 
 class MpcFulltreeProblem(ctypes.Structure):
@@ -123,6 +129,7 @@ RESULT_BYTES = ctypes.sizeof(MpcResult)
 CANDIDATE_BYTES = ctypes.sizeof(MpcCandidate)
 FT_RESULT_BYTES = ctypes.sizeof(MpcFulltreeResult)
 LOG_BYTES = ctypes.sizeof(MpcEpisodeLog)
+PROGRESS_BYTES = ctypes.sizeof(MpcEpisodesProgress)
 PROBLEM_BYTES = ctypes.sizeof(MpcProblem)
 
 STATUS_TEXT = {

@@ -22,7 +22,8 @@ struct Consts {
   double x_t, y_t;         // target globals (:65-66)
   double x_0, y_0;         // line origin globals (:57)
   double A, B, C1, C2;     // (y_t-y_0), (x_t-x_0), x_t*y_0, y_t*x_0   (:60)
-  double den;              // sqrt((y_t-y_0)**2 + (x_t-x_0)**2)        (:61)
+  double inv_den;          // 1 / sqrt((y_t-y_0)**2 + (x_t-x_0)**2)    (:61): the line
+                           // distance's division as a multiply (one rounding apart)
   double L, inv_L;         // wheelbase; 1/L when L is a power of two
   double h;                // (t+dt) - t, the quad interval length (RECT)
   double hlgth;            // 0.5*((t+dt) - t), QUADPACK's half length (QK21)
@@ -201,7 +202,10 @@ MPC_HD __forceinline__ double cost(double x, double y, const Consts& K) {
   if (x == K.x_0 && y == K.y_0) {
     d = 1000.0;                                                // :57-58
   } else {
-    d = fabs(K.A * x - K.B * y + K.C1 - K.C2) / K.den;         // :60-61
+    // :60-61, the division by the hypotenuse as a multiply by its reciprocal
+    // (formed once per problem): <= 1 ulp from the quotient, and ~10 VALU
+    // fewer per candidate than the IEEE division sequence
+    d = fabs(K.A * x - K.B * y + K.C1 - K.C2) * K.inv_den;
   }
   return 10000.0 * dist_target + 10000.0 * (d * d);            // :62, :87
 }
@@ -261,6 +265,14 @@ __device__ __forceinline__ uint64_t cost_key(double c) {
   c = c + 0.0;
   const uint64_t u = static_cast<uint64_t>(__double_as_longlong(c));
   return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+
+// cost_key for a criterion value, which is never negative (a sum of
+// 10000 * sqrt(.) and squares: +0 at least, or NaN / +inf): the same key
+// without the sign fold — 2 VALU per candidate instead of ~6.
+__device__ __forceinline__ uint64_t cost_key_nonneg(double c) {
+  const uint64_t u = static_cast<uint64_t>(__double_as_longlong(c));
+  return c < __builtin_inf() ? (u | 0x8000000000000000ull) : ~0ull;
 }
 
 __device__ __forceinline__ double key_cost(uint64_t k) {

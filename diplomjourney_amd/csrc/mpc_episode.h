@@ -294,7 +294,7 @@ __global__ __launch_bounds__(kBlock, kGenWaves) void k_rollout_generated(
         generated_lane<INTEG, ROT, PL2>(K, s_gen_grid, n_grid, seed, g0, n_steps, cst);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const uint64_t kk = cost_key(cst[j]);
+          const uint64_t kk = cost_key_nonneg(cst[j]);
           if (kk < best_k) {   // ascending index per lane: strict < keeps the first
             best_k = kk;
             best_i = c0 + j;
@@ -364,6 +364,12 @@ __device__ __forceinline__ double tr_at(const Winner& r, int k, int q) {
 // Operates on a register copy of the episode scalars (the caller loads it
 // once and stores it back once).  The step's log record is filled in `L`
 // (LDS); the caller stores it (log_slot) together with the head.
+// RESTART = false (the batched robots of mpc_episodes.h): an ended episode
+// stays ended (the caller stops the robot) instead of restarting.
+// c.stop_rule 1: run_math_model.py's stuck detector instead of math_mpc's —
+// `recursive` counts the episode's non-moving steps and the second one ends
+// it at once (:266-272, before the on-target test of the loop head).
+template <bool RESTART = true>
 __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeHead& H,
                                        StaleTraj& st, const Winner& r, mpc_episode_log_t& L) {
   EpisodeHead* S = &H;
@@ -417,12 +423,16 @@ __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeHea
   S->v = st.v;
   S->beta = st.beta;
   bool ended = false;
-  if (S->recursive) {            // :559-561 "Recursive error." -> break
+  if (c.stop_rule == 0 && S->recursive) {   // :559-561 "Recursive error." -> break
     status |= MPC_EP_BREAK;
     ended = true;
+  } else if (S->x == x_prev && S->y == y_prev && c.stop_rule == 1 && S->recursive >= 1) {
+    S->recursive += 1;                      // run_math_model.py:266-272: k == 2
+    status |= MPC_EP_STUCK | MPC_EP_BREAK;
+    ended = true;
   } else {
-    if (S->x == x_prev && S->y == y_prev) {   // :562-563
-      S->recursive = 1;
+    if (S->x == x_prev && S->y == y_prev) {   // :562-563 (stop_rule 1: k += 1)
+      S->recursive += 1;
       status |= MPC_EP_STUCK;
     }
     double tx, ty;
@@ -468,7 +478,10 @@ __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeHea
   L.v = S->v;
   L.beta = S->beta;
   L.status = status;
-  if (ended) episode_restart(c, *S);
+  if (ended) {
+    if constexpr (!RESTART) return;
+    episode_restart(c, *S);
+  }
   episode_prepare(c, *S);
 }
 
@@ -757,7 +770,7 @@ __device__ __forceinline__ Consts consts_from_words(const uint32_t* w) {
   K.B = d(offsetof(Consts, B));
   K.C1 = d(offsetof(Consts, C1));
   K.C2 = d(offsetof(Consts, C2));
-  K.den = d(offsetof(Consts, den));
+  K.inv_den = d(offsetof(Consts, inv_den));
   K.L = d(offsetof(Consts, L));
   K.inv_L = d(offsetof(Consts, inv_L));
   K.h = d(offsetof(Consts, h));
@@ -856,9 +869,18 @@ __global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
     return;
   }
   constexpr int CPL = 2;
-  __shared__ uint32_t s_w[kPubWords], s_tag[kPubWords];
+  __shared__ __attribute__((aligned(16))) uint32_t s_w[kPubWords];
+  __shared__ uint32_t s_tag[kPubWords];
   __shared__ int s_final;
-  Consts Kl, K;
+  // The step's final constants as the tile's epilogue reads them (the pose
+  // transform, the criterion, an irregular candidate's recompute): straight
+  // from the published words in LDS (s_w holds Consts' dwords), as VGPR
+  // operands loaded where they are used.  Formed in SGPRs (readfirstlane)
+  // they did not fit beside the loop's trig coefficients and spilled to VGPR
+  // lanes: ~100 v_writelane / v_readlane per wave and tile.
+  static_assert(offsetof(Consts, x) == 0 && alignof(Consts) <= 16, "Consts over s_w");
+  const Consts& K = *reinterpret_cast<const Consts*>(s_w);
+  Consts Kl;
   bool waited = false;
   // After the block's first control loads are in flight: the loop constants.
   // (K itself is formed only after the loop, from the LDS words, so that it
@@ -924,7 +946,6 @@ __global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
       }
       __syncthreads();
     }
-    K = consts_from_words(s_w);
   };
   // 32-bit candidate indices (the aligned path's rows are < 2^28 candidates,
   // wide_ok): the clamp below is one v_min with a scalar operand, no 64-bit
@@ -943,11 +964,10 @@ __global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
     // registers more (as the rect+cum stream kernel)
     rollout_lane_glds_k<INTEG, ROT, PL2, decltype(wait), decltype(pre0), decltype(mid),
                         false>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0, mid);
-    Kl = K;            // later tiles: the final constants
     if (c0 < n32) {
 #pragma unroll
       for (int j = 0; j < CPL; ++j) {
-        const uint64_t kk = cost_key(cst[j]);
+        const uint64_t kk = cost_key_nonneg(cst[j]);
         if (kk < best_k) {
           best_k = kk;
           best_i = c0 + j;

@@ -45,7 +45,7 @@ MPC_HD __forceinline__ double cost_fulltree(double x, double y, double ph, const
   if (x == K.x_0 && y == K.y_0) {
     d = 1000.0;
   } else {
-    d = fabs(K.A * x - K.B * y + K.C1 - K.C2) / K.den;
+    d = fabs(K.A * x - K.B * y + K.C1 - K.C2) * K.inv_den;   // (mpc_device.h cost)
   }
   return 10000.0 * dist_target + 10.0 * (a * a) + 100.0 * (d * d);
 }
@@ -123,7 +123,7 @@ __device__ __forceinline__ void ft_leaves_body(const Consts& K, double atan_t,
     for (int64_t k2 = k2_lo; k2 < k2_hi; ++k2) {   // wave-uniform control
       const FtCtl u = ctl[k2];
       const FtState lf = ft_apply<INTEG, ROT>(l1, u, K);
-      const uint64_t kk = cost_key(cost_fulltree(lf.x, lf.y, lf.ph, K, atan_t));
+      const uint64_t kk = cost_key_nonneg(cost_fulltree(lf.x, lf.y, lf.ph, K, atan_t));
       const int64_t j = j0 + k2;
       if (live && rec_less(kk, j, best_k, best_i)) {
         best_k = kk;

@@ -69,6 +69,42 @@ __device__ __forceinline__ void block_argmin(uint64_t& k, int64_t& i) {
   }
 }
 
+// Block-uniform constants computed on the VALU (consts_from_problem) moved to
+// SGPRs: hipcc keeps VALU results in VGPRs even when every lane holds the same
+// value, which costs the batched kernel its fifth wave (120 VGPRs -> spills).
+__device__ __forceinline__ double uniform_d(double a) {
+  const uint64_t u = static_cast<uint64_t>(__double_as_longlong(a));
+  const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(u)));
+  const uint64_t hi =
+      static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(u >> 32)));
+  return __longlong_as_double(static_cast<long long>((hi << 32) | lo));
+}
+
+__device__ __forceinline__ Consts uniform_consts(const Consts& k) {
+  Consts K;
+  K.x = uniform_d(k.x);
+  K.y = uniform_d(k.y);
+  K.phi = uniform_d(k.phi);
+  K.x_t = uniform_d(k.x_t);
+  K.y_t = uniform_d(k.y_t);
+  K.x_0 = uniform_d(k.x_0);
+  K.y_0 = uniform_d(k.y_0);
+  K.A = uniform_d(k.A);
+  K.B = uniform_d(k.B);
+  K.C1 = uniform_d(k.C1);
+  K.C2 = uniform_d(k.C2);
+  K.inv_den = uniform_d(k.inv_den);
+  K.L = uniform_d(k.L);
+  K.inv_L = uniform_d(k.inv_L);
+  K.h = uniform_d(k.h);
+  K.hlgth = uniform_d(k.hlgth);
+  K.s0 = uniform_d(k.s0);
+  K.c0 = uniform_d(k.c0);
+  K.L_pow2 = __builtin_amdgcn_readfirstlane(k.L_pow2);
+  K.pad_ = 0;
+  return K;
+}
+
 // Rollout of CPL adjacent candidates starting at column c0; costs in cst.
 template <int CPL, int INTEG, int ROT, bool STATES, bool PL2>
 __device__ __forceinline__ void rollout_lane_l(const Consts& K, const double* __restrict__ v,
@@ -350,8 +386,10 @@ __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Const
       // turns out different — an episode restart reset t — the loop runs again)
       if (pass == 0) pre();
       if constexpr (!std::is_same_v<Pre, NoPre>) {
-        if (KL.h != K.h) {   // rare (episode restart); uniform over the block
-          KL = K;
+        // (the chained step's K lives in LDS: its h and, on the rare rerun,
+        // the loop's terms are moved to SGPRs; nothing else of K is)
+        if (KL.h != uniform_d(K.h)) {   // rare (episode restart); uniform over the block
+          KL = uniform_consts(K);
           continue;
         }
       }
@@ -361,16 +399,26 @@ __device__ __forceinline__ void rollout_lane_glds_k(const Consts& K, const Const
     }
     break;
   }
+  // The criterion first (an irregular candidate's value is replaced below),
+  // then the rare recompute: nothing of the criterion (the target and line
+  // terms of K, which the chained step reads from LDS into VGPRs) is live
+  // across the recompute's register-hungry trig.
 #pragma unroll
-  for (int j = 0; j < CPL; ++j) {
-    if (bad[j]) {
-      x[j] = K.x;
-      y[j] = K.y;
-      ph[j] = K.phi;
-      for (int sr = 0; sr < n_steps; ++sr)
-        step_safe<INTEG>(x[j], y[j], ph[j], v[sr * ld + c0 + j], b[sr * ld + c0 + j], K);
+  for (int j = 0; j < CPL; ++j) cst[j] = cost(x[j], y[j], K);
+  if (bad[0] || bad[1]) {
+    // (wave-uniform SGPR copies: the recompute's trig needs the VGPRs)
+    const Consts Ks = uniform_consts(K);
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      if (bad[j]) {
+        x[j] = Ks.x;
+        y[j] = Ks.y;
+        ph[j] = Ks.phi;
+        for (int sr = 0; sr < n_steps; ++sr)
+          step_safe<INTEG>(x[j], y[j], ph[j], v[sr * ld + c0 + j], b[sr * ld + c0 + j], Ks);
+        cst[j] = cost(x[j], y[j], Ks);
+      }
     }
-    cst[j] = cost(x[j], y[j], K);
   }
 }
 
@@ -420,7 +468,7 @@ __device__ __forceinline__ void rollout_argmin_body(
       rollout_lane<CPL, INTEG, ROT, STATES>(K, v, b, n_cand, c0, n_steps, cst, states, n_cand);
 #pragma unroll
       for (int j = 0; j < CPL; ++j) {
-        const uint64_t kk = cost_key(cst[j]);
+        const uint64_t kk = cost_key_nonneg(cst[j]);
         if (kk < best_k) {  // ascending index per lane: strict < keeps the first
           best_k = kk;
           best_i = c0 + j;
@@ -1032,7 +1080,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_rollout_episode(
       rollout_lane<CPL, INTEG, ROT, false>(K, v, b, n_cand, c0, n_steps, cst, nullptr, n_cand);
 #pragma unroll
       for (int j = 0; j < CPL; ++j) {
-        const uint64_t kk = cost_key(cst[j]);
+        const uint64_t kk = cost_key_nonneg(cst[j]);
         if (kk < best_k) {
           best_k = kk;
           best_i = c0 + j;
@@ -1078,7 +1126,7 @@ __device__ __forceinline__ Consts consts_from_problem(const mpc_problem_t& p) {
   K.B = p.x_t - p.x_0;
   K.C1 = p.x_t * p.y_0;
   K.C2 = p.y_t * p.x_0;
-  K.den = sqrt(K.A * K.A + K.B * K.B);
+  K.inv_den = 1.0 / sqrt(K.A * K.A + K.B * K.B);
   K.L = p.L;
   int e;
   const double m = frexp(p.L, &e);
@@ -1087,42 +1135,6 @@ __device__ __forceinline__ Consts consts_from_problem(const mpc_problem_t& p) {
   K.h = p.t_b - p.t_a;
   K.hlgth = 0.5 * (p.t_b - p.t_a);
   trig::sincos_fast(p.phi, &K.s0, &K.c0);
-  K.pad_ = 0;
-  return K;
-}
-
-// Block-uniform constants computed on the VALU (consts_from_problem) moved to
-// SGPRs: hipcc keeps VALU results in VGPRs even when every lane holds the same
-// value, which costs the batched kernel its fifth wave (120 VGPRs -> spills).
-__device__ __forceinline__ double uniform_d(double a) {
-  const uint64_t u = static_cast<uint64_t>(__double_as_longlong(a));
-  const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(u)));
-  const uint64_t hi =
-      static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(u >> 32)));
-  return __longlong_as_double(static_cast<long long>((hi << 32) | lo));
-}
-
-__device__ __forceinline__ Consts uniform_consts(const Consts& k) {
-  Consts K;
-  K.x = uniform_d(k.x);
-  K.y = uniform_d(k.y);
-  K.phi = uniform_d(k.phi);
-  K.x_t = uniform_d(k.x_t);
-  K.y_t = uniform_d(k.y_t);
-  K.x_0 = uniform_d(k.x_0);
-  K.y_0 = uniform_d(k.y_0);
-  K.A = uniform_d(k.A);
-  K.B = uniform_d(k.B);
-  K.C1 = uniform_d(k.C1);
-  K.C2 = uniform_d(k.C2);
-  K.den = uniform_d(k.den);
-  K.L = uniform_d(k.L);
-  K.inv_L = uniform_d(k.inv_L);
-  K.h = uniform_d(k.h);
-  K.hlgth = uniform_d(k.hlgth);
-  K.s0 = uniform_d(k.s0);
-  K.c0 = uniform_d(k.c0);
-  K.L_pow2 = __builtin_amdgcn_readfirstlane(k.L_pow2);
   K.pad_ = 0;
   return K;
 }
@@ -1147,7 +1159,7 @@ k_rollout_argmin_batched(
       rollout_lane<CPL, INTEG, ROT, false>(K, v, b, ld, r * cand + cl, n_steps, cst, nullptr, 0);
 #pragma unroll
       for (int j = 0; j < CPL; ++j) {
-        const uint64_t kk = cost_key(cst[j]);
+        const uint64_t kk = cost_key_nonneg(cst[j]);
         if (kk < best_k) {
           best_k = kk;
           best_i = cl + j;

@@ -17,6 +17,7 @@
 #include "../../include/mpc_rollout.h"
 #include "mpc_comm.h"
 #include "mpc_episode.h"
+#include "mpc_episodes.h"
 #include "mpc_fulltree.h"
 #include "mpc_kernels.h"
 
@@ -44,7 +45,7 @@ Consts host_consts(const mpc_problem_t& p) {
   K.B = p.x_t - p.x_0;
   K.C1 = p.x_t * p.y_0;
   K.C2 = p.y_t * p.x_0;
-  K.den = sqrt(g_libm_pow(K.A, 2.0) + g_libm_pow(K.B, 2.0));
+  K.inv_den = 1.0 / sqrt(g_libm_pow(K.A, 2.0) + g_libm_pow(K.B, 2.0));
   K.L = p.L;
   int e;
   K.L_pow2 = (frexp(p.L, &e) == 0.5) ? 1 : 0;
@@ -196,7 +197,8 @@ void launch_finalize(hipStream_t st, int32_t integrator, const Rec* part, int n_
 int check_episode_cfg(const mpc_episode_config_t* c) {
   if (!c) return MPC_ERR_ARG;
   if (!(c->ratio_v >= 0) || !(c->ratio_beta >= 0) || c->ratio_v > 1000 || c->ratio_beta > 1000 ||
-      c->max_steps < 0 || !(c->delta_t > 0) || (c->enumerate != 0 && c->enumerate != 1))
+      c->max_steps < 0 || !(c->delta_t > 0) || (c->enumerate != 0 && c->enumerate != 1) ||
+      (c->stop_rule != 0 && c->stop_rule != 1))
     return MPC_ERR_ARG;
   return MPC_OK;
 }
@@ -741,6 +743,50 @@ int mpc_episode_advance(const mpc_episode_config_t* cfg, void* state, const mpc_
     return MPC_ERR_ARG;
   k_episode_advance<<<1, 64, 0, reinterpret_cast<hipStream_t>(stream)>>>(
       *cfg, static_cast<EpisodeState*>(state), results, n_results, log, log_capacity);
+  return last_hip_status();
+}
+
+// ----------------------------- batched episodes ----------------------------
+size_t mpc_episodes_state_bytes(int32_t n_robots) {
+  if (n_robots < 1) return 0;
+  return episodes_cfg_offset(n_robots) + static_cast<size_t>(n_robots) * sizeof(mpc_episode_config_t);
+}
+
+int mpc_episodes_reset(const mpc_episode_config_t* cfgs, int32_t n_robots, void* state,
+                       mpc_stream_t stream) {
+  if (!cfgs || !state || n_robots < 1 || n_robots > 65535) return MPC_ERR_ARG;
+  for (int32_t r = 0; r < n_robots; ++r)
+    if (check_episode_cfg(&cfgs[r]) != MPC_OK) return MPC_ERR_ARG;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  char* s = static_cast<char*>(state);
+  mpc_episode_config_t* dcfg = reinterpret_cast<mpc_episode_config_t*>(s + episodes_cfg_offset(n_robots));
+  // (pageable host source: the copy has read it when the call returns)
+  if (hipMemcpyAsync(dcfg, cfgs, static_cast<size_t>(n_robots) * sizeof(mpc_episode_config_t),
+                     hipMemcpyHostToDevice, st) != hipSuccess)
+    return MPC_ERR_HIP;
+  k_episodes_reset<<<static_cast<unsigned>(cdiv(n_robots, 256)), 256, 0, st>>>(
+      dcfg, n_robots, reinterpret_cast<RobotState*>(s));
+  return last_hip_status();
+}
+
+int mpc_episodes_run(void* state, int32_t n_robots, int32_t n_steps, int32_t integrator,
+                     int32_t max_calls, mpc_episode_log_t* log, int32_t log_capacity,
+                     mpc_episodes_progress_t* progress, mpc_stream_t stream) {
+  if (!state || n_robots < 1 || n_robots > 65535 || n_steps < 1 || n_steps > MPC_MAX_STEPS ||
+      max_calls < 0 || log_capacity < 0 || (log && log_capacity < 1))
+    return MPC_ERR_ARG;
+  if (mode_ok(integrator) != MPC_OK) return MPC_ERR_UNSUPPORTED;
+  if (max_calls == 0) return MPC_OK;
+  char* s = static_cast<char*>(state);
+  const mpc_episode_config_t* dcfg =
+      reinterpret_cast<const mpc_episode_config_t*>(s + episodes_cfg_offset(n_robots));
+  dispatch_mode(integrator, [&](auto integ, auto rot) {
+    constexpr int I = decltype(integ)::value;
+    constexpr int R = decltype(rot)::value;
+    k_episodes_run<I, R><<<n_robots, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        dcfg, reinterpret_cast<RobotState*>(s), n_steps, max_calls, log, log ? log_capacity : 0,
+        progress);
+  });
   return last_hip_status();
 }
 

@@ -520,3 +520,98 @@ def percentile(xs, q):
     s = sorted(xs)
     i = min(len(s) - 1, max(0, int(round(q / 100.0 * (len(s) - 1)))))
     return s[i]
+
+
+# numpy view of mpc_episode_log_t (include/mpc_rollout.h), 80 bytes
+_LOG_DTYPE = [("step", "<i8"), ("index", "<i8"), ("p", "<i4"), ("episode", "<i4"),
+              ("found", "<i4"), ("status", "<i4"), ("cost", "<f8"), ("x", "<f8"), ("y", "<f8"),
+              ("phi", "<f8"), ("v", "<f8"), ("beta", "<f8")]
+
+
+class DeviceEpisodes:
+    """R robots' MPC episodes in HBM (mpc_episodes_*, csrc/mpc_episodes.h):
+    one block per robot runs its episode's MPC steps back to back — the grid
+    around its control, the reference's enumeration of the step's |V| x |B|
+    constant sequences, the N-step rollout, the strict-< first minimum, the
+    winner's layer states and the episode update — so `run(k)` is ONE launch
+    for up to k MPC steps of every robot, with no host round trip and no
+    lockstep.  cfgs: one MpcEpisodeConfig per robot (start, target and rules:
+    `tree_episode_config` for run_math_model.py's loop, the reference_episode_
+    config of math_mpc for the operator scenario)."""
+
+    def __init__(self, engine, cfgs, n_steps=3, integrator="qk21", log_capacity=1024):
+        from .abi import INTEGRATORS, PROGRESS_BYTES
+        self.eng = engine
+        self.lib = native.lib()
+        self.cfgs = list(cfgs)
+        self.R = len(self.cfgs)
+        self.n_steps = int(n_steps)
+        self.integrator = integrator
+        self._integ = INTEGRATORS[integrator]
+        dev = engine.device
+        self.state = torch.zeros(self.lib.mpc_episodes_state_bytes(self.R), dtype=torch.uint8,
+                                 device=dev)
+        self.log_capacity = int(log_capacity)
+        self.log = torch.zeros(self.R * self.log_capacity * LOG_BYTES, dtype=torch.uint8,
+                               device=dev)
+        self.progress = torch.zeros(self.R * PROGRESS_BYTES, dtype=torch.uint8, device=dev)
+        self.reset()
+
+    def reset(self):
+        arr = (MpcEpisodeConfig * self.R)(*self.cfgs)
+        native.check(self.lib.mpc_episodes_reset(ctypes.byref(arr), self.R, self.state.data_ptr(),
+                                                 _stream()), "mpc_episodes_reset")
+        self.progress.zero_()
+
+    def run(self, max_calls):
+        """Enqueue up to max_calls MPC steps of every still-running robot."""
+        native.check(self.lib.mpc_episodes_run(
+            self.state.data_ptr(), self.R, self.n_steps, self._integ, int(max_calls),
+            self.log.data_ptr(), self.log_capacity, self.progress.data_ptr(), _stream()),
+            "mpc_episodes_run")
+
+    def read_progress(self):
+        """(calls, stop, candidates) per robot (numpy arrays; syncs)."""
+        import numpy as np
+        raw = self.progress.cpu().numpy()
+        p = np.frombuffer(raw.tobytes(), dtype=[("calls", "<i4"), ("stop", "<i4"),
+                                                ("candidates", "<i8")])
+        return p["calls"].copy(), p["stop"].copy(), p["candidates"].copy()
+
+    def read_logs(self, first_step=None):
+        """Per robot, its log records (numpy structured array, mpc_episode_log_t
+        fields) of steps [first, calls): first = first_step[r] if given, else
+        everything still in the ring (the last log_capacity steps)."""
+        import numpy as np
+        calls, _, _ = self.read_progress()
+        raw = np.frombuffer(self.log.cpu().numpy().tobytes(), dtype=_LOG_DTYPE)
+        raw = raw.reshape(self.R, self.log_capacity)
+        out = []
+        for r in range(self.R):
+            n = int(calls[r])
+            lo = max(0, n - self.log_capacity)
+            if first_step is not None:
+                lo = max(lo, int(first_step[r]))
+            out.append(raw[r, [s % self.log_capacity for s in range(lo, n)]])
+        return out
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def tree_episode_config(start, max_calls=None):
+    """mpc_episode_config_t of one run_math_model.py episode (:231-280) whose
+    MPC step is math_model_tree.py's tree expansion (SURVEY Fact 2): start =
+    (x_0, y_0, phi_0, x_t, y_t) as draw_starts() draws them, v = beta = 0
+    (:233-234); the reference's grid constants and enumeration; the first
+    incumbent from the start with the episode's target (:252); no operator
+    events; the script's stuck rule (the second non-moving step stops it,
+    :266-272); max_calls (None: none) as the step limit."""
+    x0, y0, phi0, xt, yt = start
+    c = reference_episode_config(start=(float(x0), float(y0), float(phi0), 0.0, 0.0),
+                                 target=(float(xt), float(yt)), max_steps=max_calls or 0,
+                                 enumerate=True)
+    c.p_turn_right = c.p_turn_left = c.p_new_target = 0
+    c.stop_rule = 1
+    return c

@@ -38,6 +38,7 @@ EXPORTS = (
     "mpc_episode_generate_workspace_bytes", "mpc_episode_generate_step",
     "mpc_fulltree_workspace_bytes", "mpc_fulltree_argmin",
     "mpc_fulltree_batched_workspace_bytes", "mpc_fulltree_argmin_batched",
+    "mpc_episodes_state_bytes", "mpc_episodes_reset", "mpc_episodes_run",
 )
 
 HIPCC_FLAGS = [
@@ -186,6 +187,12 @@ def lib():
     L.mpc_episode_rollout.restype = ctypes.c_int
     L.mpc_episode_rollout.argtypes = [_P, _P, _P, _I64, _I32, _I64, _I32, _P, ctypes.c_size_t,
                                       _P, ctypes.POINTER(MpcEpisodeConfig), _P, _I32, _P]
+    L.mpc_episodes_state_bytes.restype = ctypes.c_size_t
+    L.mpc_episodes_state_bytes.argtypes = [_I32]
+    L.mpc_episodes_reset.restype = ctypes.c_int
+    L.mpc_episodes_reset.argtypes = [_P, _I32, _P, _P]
+    L.mpc_episodes_run.restype = ctypes.c_int
+    L.mpc_episodes_run.argtypes = [_P, _I32, _I32, _I32, _I32, _P, _I32, _P, _P]
     _lib = L
     return L
 

@@ -309,9 +309,6 @@ def is_on_target_of(r):
 # and beta are reset too here, so that episodes are independent and can run
 # side by side (the script leaks them from one episode into the next).
 
-TREE_CAND = 11 * 41        # the largest acceleration-limited grid (:239-256)
-
-
 def _tree_globals(start):
     from . import math_model_tree as mmt
     x0, y0, phi0, xt, yt = start
@@ -350,131 +347,55 @@ def run_tree_episode(start, max_calls=None):
     return records, "on_target"
 
 
-def _tree_grids(v, b):
-    """vector_of_velocities / vector_of_beta_angles (:239-256) of R robots at
-    once (numpy float64, the same operations in the same order), compacted,
-    and the reference's enumeration k = a |B| + b over them padded to
-    TREE_CAND with NaN controls.  Returns (v_cand, b_cand) [R, TREE_CAND]."""
-    from . import math_model_tree as mmt
-    R = len(v)
-    rv = (mmt.v_acc_max * mmt.delta_t) / mmt.delta_v
-    iv = np.arange(1 + 2 * int(rv), dtype=np.float64)
-    cv = v[:, None] + mmt.delta_v * (iv[None, :] - rv)
-    okv = ~(cv < 0) & (cv < mmt.v_max)
-    rb = (math.degrees(mmt.beta_acc_max) * mmt.delta_t) / math.degrees(mmt.delta_beta)
-    ib = np.arange(1 + 2 * int(rb), dtype=np.float64)
-    cb = b[:, None] + mmt.delta_beta * (ib[None, :] - rb)
-    okb = np.abs(cb) <= mmt.beta_max + math.radians(mmt.eps_beta)
-    # compaction: accepted entries first, in order (stable sort on "rejected")
-    ov = np.argsort(~okv, axis=1, kind="stable")
-    ob = np.argsort(~okb, axis=1, kind="stable")
-    Vc = np.take_along_axis(cv, ov, axis=1)
-    Bc = np.take_along_axis(cb, ob, axis=1)
-    nv = okv.sum(axis=1)
-    nb = okb.sum(axis=1)
-    k = np.arange(TREE_CAND)[None, :]
-    nbk = np.maximum(nb, 1)[:, None]
-    a = np.minimum(k // nbk, Vc.shape[1] - 1)
-    bb = k % nbk
-    valid = k < (nv * nb)[:, None]
-    rows = np.arange(R)[:, None]
-    vc = np.where(valid, Vc[rows, a], np.nan)
-    bc = np.where(valid, Bc[rows, bb], np.nan)
-    return vc, bc
-
-
-class _TreeRobot:
-    """One episode of the tree-expansion loop (the module globals of
-    math_model_tree.py and run_math_model.py, per robot)."""
-
-    def __init__(self, start):
-        from . import math_model_tree as mmt
-        self.x_0, self.y_0, self.phi_0, self.x_t, self.y_t = start
-        self.x, self.y, self.phi, self.v, self.beta = self.x_0, self.y_0, self.phi_0, 0.0, 0.0
-        saved = (mmt.x_t, mmt.y_t, mmt.x_0, mmt.y_0)
-        mmt.x_t, mmt.y_t, mmt.x_0, mmt.y_0 = self.x_t, self.y_t, self.x_0, self.y_0
-        self.incumbent = mmt.control_criterion([self.x_0, self.y_0, self.phi_0])   # :252
-        mmt.x_t, mmt.y_t, mmt.x_0, mmt.y_0 = saved
-        self.m = 0
-        self.ot = None            # optimal_trajectory[0] (3 layer states), result_v/beta
-        self.k = 0
-        self.prev = (self.x, self.y)
-        self.records = []
-        self.stop = None
-
-
-def run_tree_batched(starts, max_calls=None, integrator="qk21", engine=None, stats=None):
+def run_tree_batched(starts, max_calls=None, integrator="qk21", engine=None, stats=None,
+                     chunk=1024):
     """The tree-expansion episode loop for len(starts) episodes at once, one
-    robot per episode in lockstep: every MPC step of all running episodes is
-    ONE batched launch pair (mpc_rollout_argmin_batched — config E's kernel,
-    robot = blockIdx.y, per-robot problem constants and incumbent on the
-    device) over [3, R x 451] candidate controls (each robot's grid around its
-    own (v, beta), the reference's enumeration, NaN padding), then each
-    robot's post-processing on the host.  Returns [(records, stop)] per
-    episode, as run_tree_episode returns them.  stats (optional dict) receives
-    the lockstep steps and the candidates rolled out (padding excluded)."""
-    from . import math_model_tree as mmt
-    from .abi import make_problem
-    from .expansion import problems_to_device, results_from_device
+    robot per episode, device-resident (episode.DeviceEpisodes,
+    mpc_episodes_run): each robot is one block that runs its episode's MPC
+    steps back to back — its grid around its own (v, beta), the reference's
+    enumeration, the expansion, the winner, the finishing logic m, the two-
+    non-move stop and the on-target test, all on the device — `chunk` steps
+    per launch, the log read back once per launch.  Returns [(records, stop)]
+    per episode, as run_tree_episode returns them (the script's TypeError if
+    an episode's first call finds no winner).  stats (optional dict) receives
+    the lockstep-equivalent steps (the longest episode's calls) and the
+    candidates rolled out (each call's |V| x |B|)."""
+    import numpy as np
+    from .abi import MPC_EP_ARRIVED, MPC_EP_BREAK
+    from .episode import DeviceEpisodes, tree_episode_config
     eng = engine or _device()[0]
-    robots = [_TreeRobot(s) for s in starts]
-    t = 0
-    maxsize = float(__import__("sys").maxsize)
+    R = len(starts)
+    if max_calls == 0:
+        return [([], "on_target" if is_on_target(s[0], s[1], s[3], s[4]) else "max_calls")
+                for s in starts]
+    cap = min(chunk, max_calls) if max_calls else chunk
+    eps = DeviceEpisodes(eng, [tree_episode_config(s, max_calls) for s in starts], 3, integrator,
+                         log_capacity=cap)
+    records = [[] for _ in range(R)]
+    found_any = np.zeros(R, dtype=bool)
     while True:
-        live = []
-        for r in robots:
-            if r.stop is not None:
+        eps.run(cap)
+        logs = eps.read_logs(first_step=[len(r) for r in records])
+        calls, stop, cands = eps.read_progress()
+        for r, lg in enumerate(logs):
+            if len(lg) == 0:
                 continue
-            if is_on_target(r.x, r.y, r.x_t, r.y_t):
-                r.stop = "on_target"
-            elif max_calls is not None and len(r.records) == max_calls:
-                r.stop = "max_calls"
-            else:
-                live.append(r)
-        if not live:
-            break
-        t += delta_t                                                # :302
-        R = len(live)
-        vc, bc = _tree_grids(np.array([r.v for r in live], dtype=np.float64),
-                             np.array([r.beta for r in live], dtype=np.float64))
-        if stats is not None:
-            stats["steps"] = stats.get("steps", 0) + 1
-            stats["candidates"] = stats.get("candidates", 0) + int((~np.isnan(vc)).sum())
-        v_sc = torch.from_numpy(np.ascontiguousarray(vc.reshape(1, -1))).to(eng.device)
-        b_sc = torch.from_numpy(np.ascontiguousarray(bc.reshape(1, -1))).to(eng.device)
-        v_sc = v_sc.expand(3, -1).contiguous()
-        b_sc = b_sc.expand(3, -1).contiguous()
-        probs = problems_to_device([make_problem(r.x, r.y, r.phi, r.x_t, r.y_t, r.x_0, r.y_0, L,
-                                                 t, t + delta_t) for r in live], eng.device)
-        inc = torch.tensor([r.incumbent for r in live], dtype=torch.float64, device=eng.device)
-        res = results_from_device(eng.rollout_argmin_batched(probs, v_sc, b_sc, TREE_CAND,
-                                                             incumbents_dev=inc,
-                                                             integrator=integrator))
-        for r, w in zip(live, res):
-            if w.found:                                             # :351-359
-                tr = w.trajectory()
-                r.ot = ([list(tr[0]), list(tr[1]), list(tr[2])], w.v, w.beta)
-            if r.ot is None:
+            f = lg["found"] != 0
+            if not found_any[r] and not f[0]:
                 raise TypeError("'int' object is not subscriptable")   # [[[0]]], as the script
-            r.incumbent = maxsize                                   # :428
-            ot, rv, rb = r.ot
-            kk = 0                                                  # :392-414
-            if r.m == 2:
-                kk = 2
-            elif r.m == 1:
-                kk = 1
-                r.m += 1
-            elif mmt.is_on_target(ot[2][0], ot[2][1], r.x_t, r.y_t)[0]:
-                r.m += 1
-            c = [ot[kk][0], ot[kk][1], ot[kk][2], rv, rb]
-            r.records.append(c)
-            r.x, r.y, r.phi, r.v, r.beta = c
-            if r.x == r.prev[0] and r.y == r.prev[1]:             # :268-272
-                r.k += 1
-            if r.k == 2:
-                r.stop = "recursive_error"
-            r.prev = (r.x, r.y)
-    return [(r.records, r.stop) for r in robots]
+            found_any[r] |= bool(f.any())
+            records[r].extend(np.stack([lg["x"], lg["y"], lg["phi"], lg["v"], lg["beta"]],
+                                       axis=1).tolist())
+        if (stop != 0).all():
+            break
+    if stats is not None:
+        stats["steps"] = stats.get("steps", 0) + int(calls.max(initial=0))
+        stats["candidates"] = stats.get("candidates", 0) + int(cands.sum())
+    names = []
+    for st in stop:
+        names.append("recursive_error" if st & MPC_EP_BREAK else
+                     "on_target" if st & MPC_EP_ARRIVED else "max_calls")
+    return [(records[r], names[r]) for r in range(R)]
 
 
 __all__ = ["configure", "shard_over", "draw_starts", "run_batched", "is_on_target",

@@ -228,7 +228,10 @@ typedef struct mpc_episode_config {
                               k < |V|*|B| is the constant sequence (V[k / |B|], B[k % |B|])
                               (:311-317), candidates beyond the step's grid are padding with
                               NaN controls (never chosen); 0 = constant prefix + hashed rest */
-  int32_t reserved_;
+  int32_t stop_rule;       /* the stuck detector: 0 = math_mpc's (a step that returns the
+                              previous pose sets `recursive`, the next step ends the episode,
+                              math_model_tree.py:559-563); 1 = run_math_model.py's (the
+                              episode's second non-moving step ends it, :266-272)           */
   uint64_t seed;                                           /* candidate sampler seed       */
 } mpc_episode_config_t;
 
@@ -385,6 +388,39 @@ int mpc_episode_generate_step(const mpc_episode_config_t* cfg, void* state, int6
  * collection of its block records timed out (`local` then holds none).
  * Reads the device state (syncs). */
 int mpc_episode_chain_error(const void* state, int32_t* error, mpc_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Batched device-resident episodes: run_math_model.py's loop
+ * (:231-280) over R robots — each its own episode (start, target, rules in
+ * its mpc_episode_config_t) whose MPC step is math_model_tree.py's tree
+ * expansion: the grid around the robot's (v, beta) (:239-256, slow-down
+ * :312-316), the reference's enumeration of its |V|*|B| constant sequences
+ * (:308-350, at most 64 x 64), the n_steps-layer rollout, the strict-< first
+ * minimum against the robot's incumbent (:351), the winner's layer states, the
+ * update of mpc_episode_advance (finishing logic, cfg.stop_rule's stuck
+ * detector, events when enabled, arrival, cfg.max_steps) — without restart: an
+ * ended episode stops its robot.  ONE launch runs up to max_calls MPC steps of
+ * every robot (one block per robot, no host round trip, no lockstep);
+ * repeated launches continue the episodes.  cfg.enumerate is implied.
+ *   mpc_episodes_reset   copies the R configurations (host array, validated)
+ *                        into the state and starts every episode (a robot that
+ *                        starts on its target is stopped at once)
+ *   mpc_episodes_run     log: [R][log_capacity] rings of mpc_episode_log_t
+ *                        (slot = step % capacity, nullable); progress: device
+ *                        array [R], written at the end of the launch
+ * ------------------------------------------------------------------------- */
+typedef struct mpc_episodes_progress {
+  int32_t calls;         /* MPC steps run so far                                     */
+  int32_t stop;          /* 0 = running; else the MPC_EP_* bits of the step that ended
+                            the episode (MPC_EP_ARRIVED with calls 0: started on target) */
+  int64_t candidates;    /* candidates rolled out so far (sum of the steps' |V|*|B|)   */
+} mpc_episodes_progress_t;
+size_t mpc_episodes_state_bytes(int32_t n_robots);
+int mpc_episodes_reset(const mpc_episode_config_t* cfgs, int32_t n_robots, void* state,
+                       mpc_stream_t stream);
+int mpc_episodes_run(void* state, int32_t n_robots, int32_t n_steps, int32_t integrator,
+                     int32_t max_calls, mpc_episode_log_t* log, int32_t log_capacity,
+                     mpc_episodes_progress_t* progress, mpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Full-tree MPC of run_math_model.py / math_model.py.

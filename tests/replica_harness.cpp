@@ -61,7 +61,7 @@ extern "C" int replica_rollout(const mpc_problem_t* p, const double* v, const do
   K.A = p->y_t - p->y_0; K.B = p->x_t - p->x_0;
   K.C1 = p->x_t * p->y_0; K.C2 = p->y_t * p->x_0;
   double (*volatile pw)(double, double) = pow;
-  K.den = sqrt(pw(K.A, 2.0) + pw(K.B, 2.0));
+  K.inv_den = 1.0 / sqrt(pw(K.A, 2.0) + pw(K.B, 2.0));
   K.L = p->L;
   int e;
   K.L_pow2 = frexp(p->L, &e) == 0.5;

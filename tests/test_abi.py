@@ -55,6 +55,49 @@ def test_struct_layout_matches_c(tmp_path):
                    R.found.offset, R.v.offset, R.traj.offset]
 
 
+def test_episode_struct_layouts_match_c(tmp_path):
+    """mpc_episode_config_t (incl. stop_rule), mpc_episode_log_t and
+    mpc_episodes_progress_t: the ctypes mirrors equal the C layouts."""
+    src = tmp_path / "layout2.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "mpc_rollout.h"\n'
+        "int main(void){printf(\"%zu %zu %zu %zu %zu %zu %zu\\n\", sizeof(mpc_episode_config_t),"
+        " offsetof(mpc_episode_config_t, stop_rule), offsetof(mpc_episode_config_t, seed),"
+        " sizeof(mpc_episode_log_t), sizeof(mpc_episodes_progress_t),"
+        " offsetof(mpc_episodes_progress_t, stop), offsetof(mpc_episodes_progress_t, candidates));"
+        " return 0;}\n")
+    exe = tmp_path / "layout2"
+    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), "-o", str(exe), str(src)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    C, P = abi.MpcEpisodeConfig, abi.MpcEpisodesProgress
+    assert got == [ctypes.sizeof(C), C.stop_rule.offset, C.seed.offset,
+                   ctypes.sizeof(abi.MpcEpisodeLog), ctypes.sizeof(P), P.stop.offset,
+                   P.candidates.offset]
+
+
+def test_batched_episodes_argument_validation_without_gpu():
+    """mpc_episodes_*: sizes and rejected arguments, before any HIP call."""
+    from diplomjourney_amd.episode import reference_episode_config
+    L = native.lib()
+    assert L.mpc_episodes_state_bytes(0) == 0
+    n1 = L.mpc_episodes_state_bytes(1)
+    assert L.mpc_episodes_state_bytes(1000) > 1000 * ctypes.sizeof(abi.MpcEpisodeConfig) > n1 > 0
+    fake = ctypes.c_void_p(0x1000)
+    cfg = reference_episode_config()
+    bad = reference_episode_config()
+    bad.stop_rule = 2
+    arr = (abi.MpcEpisodeConfig * 2)(cfg, bad)
+    assert L.mpc_episodes_reset(ctypes.byref(arr), 2, fake, None) == abi.MPC_ERR_ARG
+    assert L.mpc_episodes_reset(None, 1, fake, None) == abi.MPC_ERR_ARG
+    assert L.mpc_episodes_reset(ctypes.byref(arr), 0, fake, None) == abi.MPC_ERR_ARG
+    assert L.mpc_episodes_run(None, 1, 3, 0, 1, None, 0, None, None) == abi.MPC_ERR_ARG
+    assert L.mpc_episodes_run(fake, 1, 0, 0, 1, None, 0, None, None) == abi.MPC_ERR_ARG
+    assert L.mpc_episodes_run(fake, 1, 3, 0, 1, fake, 0, None, None) == abi.MPC_ERR_ARG
+    assert L.mpc_episodes_run(fake, 1, 3, 7, 1, None, 0, None, None) == abi.MPC_ERR_UNSUPPORTED
+    assert L.mpc_episodes_run(fake, 1, 3, 0, 0, None, 0, None, None) == abi.MPC_OK   # nothing
+
+
 def test_workspace_sizes():
     L = native.lib()
     assert L.mpc_workspace_bytes(1, 3) == 16

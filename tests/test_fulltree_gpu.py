@@ -193,3 +193,61 @@ def test_tree_episode_loop_batched_equals_sequential(engine):
         for a, b in zip(rs, rb):
             assert a[3:] == b[3:]
             assert max(abs(p - q) for p, q in zip(a[:3], b[:3])) <= 1e-12
+
+
+def test_tree_episodes_chunked_launches_equal_one_launch(engine):
+    """The device episodes continue across launches: the same episodes run
+    7 MPC steps per launch (the log read back after every launch) return
+    exactly what one launch per 120 steps returns."""
+    from diplomjourney_amd import run_math_model as rmm
+    starts = rmm.draw_starts(20, seed=7)
+    one = rmm.run_tree_batched(starts, max_calls=120, integrator="qk21", engine=engine)
+    many = rmm.run_tree_batched(starts, max_calls=120, integrator="qk21", engine=engine, chunk=7)
+    assert one == many
+    assert sum(len(r) for r, _ in one) > 200
+
+
+@pytest.mark.parametrize("integ", ["qk21", "rect+rot"])
+def test_batched_episodes_replay_reference_scenario_as_robot_0(engine, scenario, integ):
+    """The reference's model run (math_model_tree.py:736: math_mpc from (0, 0,
+    0) to (2, 3) with the operator events at p = 60 / 90 / 110, the first
+    incumbent of :676) as robot 0 of R = 64 batched device episodes
+    (mpc_episodes_run, one block per robot) whose other 63 robots run
+    run_math_model.py episodes: robot 0 logs the 151 recorded calls — chosen
+    (v, beta) identical, pose within 1e-6, the events and the arrival after
+    call 150 — and the other robots equal their sequential drop-in episodes."""
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd import run_math_model as rmm
+    from diplomjourney_amd.abi import MPC_EP_ARRIVED, MPC_EP_EVENT
+    from diplomjourney_amd.episode import (DeviceEpisodes, reference_episode_config,
+                                           tree_episode_config)
+    calls = [c for c in scenario["calls"] if not c["isActual"]]
+    starts = rmm.draw_starts(63, seed=11)
+    cfgs = [reference_episode_config(enumerate=True, incumbent0=10000050990.195135)]
+    cfgs += [tree_episode_config(s, 60) for s in starts]
+    eps = DeviceEpisodes(engine, cfgs, 3, integ, log_capacity=256)
+    eps.run(400)
+    n, stop, _ = eps.read_progress()
+    logs = eps.read_logs()
+    assert n[0] == len(calls) == 151 and stop[0] & MPC_EP_ARRIVED
+    worst = 0.0
+    for i, (rec, g) in enumerate(zip(calls, logs[0])):
+        assert (g["p"], g["episode"], g["found"]) == (i + 1, 1, int(rec["found"])), i
+        assert (g["v"], g["beta"]) == tuple(rec["ret"][3:5]), i
+        worst = max(worst, max(abs(a - b) for a, b in zip((g["x"], g["y"], g["phi"]),
+                                                          rec["ret"][:3])))
+        want = MPC_EP_EVENT if g["p"] in (60, 90, 110) else 0
+        want |= MPC_EP_ARRIVED if i == len(calls) - 1 else 0
+        assert g["status"] == want, (i, g["status"])
+    assert worst <= 1e-6, worst
+    if integ == "qk21":
+        try:
+            for r in (1, 2, 3, 40):
+                seq, st = rmm.run_tree_episode(starts[r - 1], max_calls=60)
+                got = logs[r]
+                assert len(seq) == len(got) == n[r]
+                for a, g in zip(seq, got):
+                    assert a[3:] == [g["v"], g["beta"]]
+                    assert max(abs(p - q) for p, q in zip(a[:3], (g["x"], g["y"], g["phi"]))) <= 1e-12
+        finally:
+            mmt.reset_state()

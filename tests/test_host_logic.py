@@ -208,24 +208,3 @@ def test_bench_spawned_rank_failure_fails_the_run():
                 "--cpu-seconds", "0"], {"DIPLOMJOURNEY_MPC_LIB": "/nonexistent/lib.so"})
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-
-
-def test_tree_grids_match_reference_enumeration():
-    """run_math_model.run_tree_batched's vectorised grids: per robot exactly
-    vector_of_velocities x vector_of_beta_angles (math_model_tree.py:239-256)
-    in the reference's k = a|B| + b order, NaN padding to 451."""
-    import numpy as np
-    from diplomjourney_amd import math_model_tree as mmt
-    from diplomjourney_amd import run_math_model as rmm
-    rng = np.random.default_rng(1)
-    v = np.concatenate([[0.0, 0.005, 1.0, 0.995, 0.4], rng.uniform(0, 1, 100)])
-    b = np.concatenate([[0.0, mmt.beta_max, -mmt.beta_max, 1.0, -1.05],
-                        rng.uniform(-1.1, 1.1, 100)])
-    vc, bc = rmm._tree_grids(v, b)
-    for i in range(len(v)):
-        V = mmt.vector_of_velocities(float(v[i]))
-        B = mmt.vector_of_beta_angles(float(b[i]))
-        n = len(V) * len(B)
-        assert list(vc[i, :n]) == [V[k // len(B)] for k in range(n)]
-        assert list(bc[i, :n]) == [B[k % len(B)] for k in range(n)]
-        assert np.isnan(vc[i, n:]).all() and np.isnan(bc[i, n:]).all()
