@@ -198,15 +198,12 @@ MPC_HD __forceinline__ void step_safe(double& x, double& y, double& ph, double v
 MPC_HD __forceinline__ double cost(double x, double y, const Consts& K) {
   const double ex = K.x_t - x, ey = K.y_t - y;
   const double dist_target = sqrt(ex * ex + ey * ey);          // :66
-  double d;
-  if (x == K.x_0 && y == K.y_0) {
-    d = 1000.0;                                                // :57-58
-  } else {
-    // :60-61, the division by the hypotenuse as a multiply by its reciprocal
-    // (formed once per problem): <= 1 ulp from the quotient, and ~10 VALU
-    // fewer per candidate than the IEEE division sequence
-    d = fabs(K.A * x - K.B * y + K.C1 - K.C2) * K.inv_den;
-  }
+  // :60-61, the division by the hypotenuse as a multiply by its reciprocal
+  // (formed once per problem): <= 1 ulp from the quotient, and ~10 VALU
+  // fewer per candidate than the IEEE division sequence.  Both sides of the
+  // sentinel test are formed and one selected (no divergent branch).
+  const double dl = fabs(K.A * x - K.B * y + K.C1 - K.C2) * K.inv_den;
+  const double d = (x == K.x_0 && y == K.y_0) ? 1000.0 : dl;  // :57-58
   return 10000.0 * dist_target + 10000.0 * (d * d);            // :62, :87
 }
 

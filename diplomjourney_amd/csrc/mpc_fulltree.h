@@ -28,6 +28,7 @@ namespace mpc {
 
 struct FtCtl {
   double v, beta, dphi, sd, cm1;
+  double vh;   // v * h (RECT's position increment factor, formed once per control)
 };
 
 struct FtState {
@@ -41,12 +42,8 @@ MPC_HD __forceinline__ double cost_fulltree(double x, double y, double ph, const
   const double a = atan_t - ph;
   const double ex = K.x_t - x, ey = K.y_t - y;
   const double dist_target = sqrt(ex * ex + ey * ey);
-  double d;
-  if (x == K.x_0 && y == K.y_0) {
-    d = 1000.0;
-  } else {
-    d = fabs(K.A * x - K.B * y + K.C1 - K.C2) * K.inv_den;   // (mpc_device.h cost)
-  }
+  const double dl = fabs(K.A * x - K.B * y + K.C1 - K.C2) * K.inv_den;   // (mpc_device.h cost)
+  const double d = (x == K.x_0 && y == K.y_0) ? 1000.0 : dl;
   return 10000.0 * dist_target + 10.0 * (a * a) + 100.0 * (d * d);
 }
 
@@ -64,8 +61,13 @@ MPC_HD __forceinline__ FtState ft_apply(const FtState& in, const FtCtl& u, const
   } else {
     trig::sincos_fast(o.ph, &o.s, &o.c);
   }
-  o.x = position_step<INTEG>(in.x, u.v, o.c, K);
-  o.y = position_step<INTEG>(in.y, u.v, o.s, K);
+  if constexpr (INTEG == MPC_INTEG_RECT) {   // = position_step: fma(v * h, trig, p)
+    o.x = fma(u.vh, o.c, in.x);
+    o.y = fma(u.vh, o.s, in.y);
+  } else {
+    o.x = position_step<INTEG>(in.x, u.v, o.c, K);
+    o.y = position_step<INTEG>(in.y, u.v, o.s, K);
+  }
   return o;
 }
 
@@ -79,6 +81,7 @@ __global__ __launch_bounds__(kBlock) void k_ft_controls(Consts K, const double* 
   FtCtl u;
   u.v = V[k / nb];
   u.beta = B[k % nb];
+  u.vh = u.v * K.h;
   const double w = K.L_pow2 ? u.v * K.inv_L : u.v / K.L;
   u.dphi = heading_incr<INTEG>(w, trig::tan_fast(u.beta), K);
   if (fabs(u.dphi) <= trig::kRotMax) {
@@ -124,10 +127,11 @@ __device__ __forceinline__ void ft_leaves_body(const Consts& K, double atan_t,
       const FtCtl u = ctl[k2];
       const FtState lf = ft_apply<INTEG, ROT>(l1, u, K);
       const uint64_t kk = cost_key_nonneg(cost_fulltree(lf.x, lf.y, lf.ph, K, atan_t));
-      const int64_t j = j0 + k2;
-      if (live && rec_less(kk, j, best_k, best_i)) {
+      // a lane's leaf indices only grow (items ascend, and so do (k0, k1) and
+      // k2 within them): strict < keeps its first minimum, as rec_less would
+      if (live && kk < best_k) {
         best_k = kk;
-        best_i = j;
+        best_i = j0 + k2;
       }
     }
   }
