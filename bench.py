@@ -131,6 +131,10 @@ def parse():
                     help="use the multi-GPU step structure (finalize -> RCCL all_gather -> "
                          "advance) even on one rank: rehearses the exchange and its graph "
                          "capture on a single GPU (1-rank process group)")
+    ap.add_argument("--overlap-exchange", action="store_true",
+                    help="exchange steps: run the all_gather of step k on a side stream beside "
+                         "launch k+1, whose block 0 waits for the collective's device-side mark "
+                         "(mpc_episode_exchange_step2) instead of the launch waiting for it")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks on fewer GPUs (exchange staged via host)")
     ap.add_argument("--candidates-per-gpu", type=int, default=None,
@@ -439,7 +443,8 @@ def main():
                            integrator=args.integrator, group=group, log_capacity=8192,
                            exchange=exchange, split=not args.fused,
                            chain=not args.no_chain and args.integrator == "rect+cum",
-                           generate=inputs == "generated")
+                           generate=inputs == "generated",
+                           overlap=args.overlap_exchange and exchange)
     pool = make_pool(eng, ep, n_steps, args.steps) if inputs == "resident" else None
     rollout_ms = None
     # the launch that carries the step: the chained kernel (rollout of step k +

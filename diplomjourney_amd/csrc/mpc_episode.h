@@ -42,6 +42,11 @@ struct EpisodeState {
   // the launch's epoch ((dword << 32) | epoch), so one coherent load per word
   // says whether its value is this step's.  Tag 0: none.
   alignas(128) uint64_t chain_pub[kPubWords];
+  // Overlapped exchange (mpc_episode_exchange_step2 with wait_tag): the epoch
+  // of the step whose candidates the last all_gather delivered, stored by
+  // k_exchange_mark on the collective's stream after the collective; block 0
+  // of the next launch polls it instead of the launch waiting on a stream edge.
+  alignas(128) uint64_t gathered_tag;
 };
 static_assert(offsetof(EpisodeState, st) == sizeof(EpisodeHead), "stale trajectory follows the head");
 
@@ -116,6 +121,7 @@ __global__ void k_episode_reset(mpc_episode_config_t c, EpisodeState* __restrict
   S->done = 0u;
   S->chain_error = 0u;
   for (int q = 0; q < kPubWords; ++q) S->chain_pub[q] = 0ull;
+  S->gathered_tag = 0ull;
 }
 
 // Grids (:239-256) with the reference's expressions and the slow-down
@@ -712,6 +718,55 @@ __device__ void collect_local_candidate(const Rec* __restrict__ part, int n_part
   }
 }
 
+// The overlapped exchange's hand-off: after the all_gather of step `tag`'s
+// candidates (same stream, so the collective's stores are complete), publish
+// the tag.  One coherent 8-B store (relaxed, agent scope: `sc1`).
+__global__ void k_exchange_mark(EpisodeState* __restrict__ S, uint32_t tag) {
+  if (threadIdx.x == 0) __hip_atomic_store(&S->gathered_tag, static_cast<uint64_t>(tag),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int kXchgLdsRanks = 32;   // gathered candidates staged in the ring's LDS
+static_assert(kXchgLdsRanks * sizeof(mpc_candidate_t) + sizeof(EmitLds) <= sizeof(g_ring),
+              "staged candidates + the re-roll's LDS fit in the control ring");
+
+// Block 0 of an overlapped exchange step, all threads: wait (bounded) until
+// the all_gather of step `tag` has been marked, then copy the n gathered
+// candidates into LDS with coherent 8-B loads (the collective wrote them
+// while this launch was already running: no stream edge orders them for
+// it).  Returns the LDS copy, or nullptr if the wait timed out (error 4).
+__device__ const mpc_candidate_t* wait_gathered(EpisodeState* S, uint32_t tag,
+                                                const mpc_candidate_t* __restrict__ g, int n) {
+  __shared__ int s_ok;
+  if (threadIdx.x < 64) {
+    bool ok = false;
+    for (uint32_t it = 0; it < kChainSpinLimit; ++it) {
+      const uint64_t w = __hip_atomic_load(&S->gathered_tag, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      if (static_cast<uint32_t>(w) == tag) {
+        ok = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (threadIdx.x == 0) {
+      s_ok = ok;
+      if (!ok) S->chain_error = 4u;
+    }
+  }
+  __syncthreads();
+  if (!s_ok) return nullptr;
+  mpc_candidate_t* dst = reinterpret_cast<mpc_candidate_t*>(
+      reinterpret_cast<char*>(ring_lds()) + ((sizeof(EmitLds) + 15) & ~size_t{15}));
+  const int words = n * static_cast<int>(sizeof(mpc_candidate_t) / 8);
+  for (int q = threadIdx.x; q < words; q += blockDim.x)
+    reinterpret_cast<uint64_t*>(dst)[q] =
+        __hip_atomic_load(reinterpret_cast<const uint64_t*>(g) + q, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return dst;
+}
+
 __global__ __launch_bounds__(64) void k_episode_advance(mpc_episode_config_t c,
                                                         EpisodeState* __restrict__ S,
                                                         const mpc_result_t* __restrict__ res,
@@ -832,7 +887,8 @@ __global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
     int has_prev, const Rec* __restrict__ part_prev, int n_part_prev,
     const double* __restrict__ v_prev, const double* __restrict__ b_prev, int64_t index_base,
     mpc_result_t* __restrict__ out_prev, const mpc_candidate_t* __restrict__ gathered,
-    int n_gathered, mpc_episode_config_t ecfg, mpc_episode_log_t* __restrict__ log, int cap) {
+    int n_gathered, mpc_episode_config_t ecfg, mpc_episode_log_t* __restrict__ log, int cap,
+    uint32_t wait_tag) {
   static_assert(ROT == kRotCum, "chained steps need the pose-independent recurrence");
   if (blockIdx.x == 0) {
     if (has_prev) {
@@ -847,8 +903,15 @@ __global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
                                                         S->h.incumbent, out_prev, ecfg, hook,
                                                         ring_lds());
       } else {
-        advance_from_candidates<INTEG, ROT>(ecfg, S, gathered, n_gathered, out_prev, log, cap,
-                                            epoch, ring_lds());
+        // overlapped exchange: the gathered candidates come from a collective
+        // that ran beside this launch — wait for its mark, stage them in LDS
+        const mpc_candidate_t* g =
+            wait_tag ? wait_gathered(S, wait_tag, gathered, n_gathered) : gathered;
+        if (g)
+          advance_from_candidates<INTEG, ROT>(ecfg, S, g, n_gathered, out_prev, log, cap,
+                                              epoch, ring_lds());
+        else   // timed out (chain error 4): publish the unchanged head so no tile hangs
+          chain_publish(S, epoch);
       }
       __syncthreads();   // (the wheelbase check below reads the stored head)
     } else {

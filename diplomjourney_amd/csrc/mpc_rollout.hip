@@ -585,7 +585,7 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
     k_episode_chain<I, kRotCum, kChainFin, P><<<tiles + 1, kBlock, 0, st>>>(
         S, epoch, v_sc, beta_sc, n_cand, n_steps, static_cast<Rec*>(ws), has_prev,
         static_cast<const Rec*>(ws_prev), n_part_prev, v_prev, beta_prev, index_base, out_prev,
-        nullptr, 0, *cfg, log, log_capacity);
+        nullptr, 0, *cfg, log, log_capacity, 0u);
   };
   if (pl2)
     launch(std::true_type{});
@@ -600,12 +600,27 @@ int mpc_episode_exchange_step(const mpc_episode_config_t* cfg, void* state, uint
                               size_t ws_bytes, const mpc_candidate_t* gathered,
                               int32_t n_gathered, mpc_result_t* out_prev, mpc_candidate_t* local,
                               mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream) {
+  return mpc_episode_exchange_step2(cfg, state, epoch, 0u, v_sc, beta_sc, n_cand, n_steps,
+                                    index_base, integrator, ws, ws_bytes, gathered, n_gathered,
+                                    out_prev, local, log, log_capacity, stream);
+}
+
+int mpc_episode_exchange_step2(const mpc_episode_config_t* cfg, void* state, uint32_t epoch,
+                               uint32_t wait_tag, const double* v_sc, const double* beta_sc,
+                               int64_t n_cand, int32_t n_steps, int64_t index_base,
+                               int32_t integrator, void* ws, size_t ws_bytes,
+                               const mpc_candidate_t* gathered, int32_t n_gathered,
+                               mpc_result_t* out_prev, mpc_candidate_t* local,
+                               mpc_episode_log_t* log, int32_t log_capacity,
+                               mpc_stream_t stream) {
   if (check_episode_cfg(cfg) != MPC_OK ||
       check_episode_arrays(state, v_sc, beta_sc, n_cand, n_steps) != MPC_OK || index_base < 0 ||
       log_capacity < 0 || epoch == 0 || !local || !out_prev)
     return MPC_ERR_ARG;
   // local indices travel in the low 32 bits of a tagged record
   if (n_cand > 0x7fffffffll || (gathered && n_gathered < 1)) return MPC_ERR_ARG;
+  // an overlapped step stages the gathered candidates in LDS
+  if (wait_tag && (!gathered || n_gathered > kXchgLdsRanks)) return MPC_ERR_ARG;
   if (mode_ok(integrator) != MPC_OK || !is_cum(integrator) || !wide_ok(v_sc, beta_sc, n_cand))
     return MPC_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
@@ -620,12 +635,19 @@ int mpc_episode_exchange_step(const mpc_episode_config_t* cfg, void* state, uint
     k_episode_chain<I, kRotCum, kChainXchg, P><<<grid, kBlock, 0, st>>>(
         S, epoch, v_sc, beta_sc, n_cand, n_steps, static_cast<Rec*>(ws), gathered ? 1 : 0,
         reinterpret_cast<const Rec*>(local), 0, nullptr, nullptr, index_base, out_prev, gathered,
-        n_gathered, *cfg, log, log_capacity);
+        n_gathered, *cfg, log, log_capacity, gathered ? wait_tag : 0u);
   };
   if (pl2)
     launch(std::true_type{});
   else
     launch(std::false_type{});
+  return last_hip_status();
+}
+
+int mpc_episode_exchange_mark(void* state, uint32_t tag, mpc_stream_t stream) {
+  if (!state || tag == 0) return MPC_ERR_ARG;
+  k_exchange_mark<<<1, 64, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+      static_cast<EpisodeState*>(state), tag);
   return last_hip_status();
 }
 

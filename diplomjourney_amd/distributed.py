@@ -108,3 +108,14 @@ def gather_bytes(local, group=None):
     out = torch.empty(world * local.numel(), dtype=torch.uint8, device=local.device)
     dist.all_gather_into_tensor(out, local, group=group)
     return out
+
+
+def gather_into(out, local, group=None):
+    """all_gather of one uint8 record per rank into the preallocated `out`
+    (uint8[world * len]) on the current stream (RCCL; gloo stages through
+    host memory)."""
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        out.copy_(gather_bytes(local.cpu(), group), non_blocking=True)
+        return out
+    dist.all_gather_into_tensor(out, local, group=group)
+    return out

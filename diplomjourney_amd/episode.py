@@ -28,7 +28,7 @@ from . import math_model_tree as mmt
 from .abi import (CANDIDATE_BYTES, LOG_BYTES, MPC_EP_ARRIVED, MPC_EP_BREAK, MPC_EP_EVENT,
                   MPC_EP_LIMIT, MPC_EP_STALE, MPC_EP_STUCK, RESULT_BYTES, MpcEpisodeConfig,
                   MpcEpisodeLog, make_problem)
-from .distributed import exchange_winner, gather_bytes, gather_results, shard_range
+from .distributed import exchange_winner, gather_bytes, gather_into, gather_results, shard_range
 from . import native
 
 CHAIN_ERRORS = {
@@ -38,6 +38,8 @@ CHAIN_ERRORS = {
        "launch's cfg",
     3: "an exchange launch's block 0 timed out collecting its tile records (this rank's "
        "candidate dropped out of the global arg-min)",
+    4: "an overlapped exchange launch's block 0 timed out waiting for the all_gather's mark "
+       "(the collective could not run beside the launch: the step was not completed)",
 }
 
 
@@ -247,7 +249,7 @@ class DeviceEpisode:
     def __init__(self, engine, n_cand_total, n_steps, rank=0, world=1, seed=20261015,
                  integrator="rect", group=None, start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3),
                  log_capacity=4096, split=True, exchange=None, chain=False, L=None,
-                 generate=False, max_steps=0, incumbent0=0.0, enumerate=False):
+                 generate=False, max_steps=0, incumbent0=0.0, enumerate=False, overlap=False):
         self.eng = engine
         self.lib = native.lib()
         self.n_total = int(n_cand_total)
@@ -291,6 +293,17 @@ class DeviceEpisode:
         # exchange + chain: this rank's best candidate of the step (the
         # all_gather payload of mpc_episode_exchange_step)
         self.cand = torch.zeros(CANDIDATE_BYTES, dtype=torch.uint8, device=dev)
+        # overlap (exchange + chain): the all_gather of step k runs on a side
+        # stream beside launch k+1, whose block 0 waits for its device-side
+        # mark (mpc_episode_exchange_step2 / _mark) — see include/mpc_rollout.h
+        self.overlap = bool(overlap)
+        if self.overlap and not (self.exchange and self.chain):
+            raise ValueError("overlap: the chained exchange step only (exchange=True, chain=True)")
+        if self.overlap and self.world > 32:
+            raise ValueError("overlap: at most 32 ranks (gathered candidates staged in LDS)")
+        self._gathered = torch.zeros(self.world * CANDIDATE_BYTES, dtype=torch.uint8, device=dev)
+        self._comm = torch.cuda.Stream(device=dev) if self.overlap else None
+        self._pend_epoch = 0
         # generate: steps without caller controls draw their candidates inside
         # the rollout (mpc_episode_generate_step) instead of sampling them into
         # v_sc / b_sc first — the same candidates, never written to HBM
@@ -349,7 +362,7 @@ class DeviceEpisode:
                 ws_prev.data_ptr(), ws.numel(), pv, pb, self.local.data_ptr(), None, 0,
                 self.log.data_ptr(), self.log_capacity, st), "mpc_episode_chain_step")
             self._pending = (v, b)
-        else:
+        elif not self.overlap:
             # one launch (selection of step k-1 over the gathered candidates +
             # the rollout of step k + this rank's candidate), then ONE
             # all_gather of the 536-B candidates
@@ -364,6 +377,30 @@ class DeviceEpisode:
                 events[1].record()
                 events = None
             self._pending = gather_bytes(self.cand, self.group)
+        else:
+            # the same launch, but the collective of the previous step may
+            # still be running beside it: block 0 waits for its mark
+            epoch = self._next_epoch()
+            native.check(L.mpc_episode_exchange_step2(
+                ctypes.byref(self.cfg), self.state.data_ptr(), epoch,
+                self._pend_epoch if pend is not None else 0, v.data_ptr(), b.data_ptr(),
+                self.n_local, self.n_steps, self.lo, self._integ, ws.data_ptr(), ws.numel(),
+                self._gathered.data_ptr() if pend is not None else None,
+                self.world if pend is not None else 0, self.winner.data_ptr(),
+                self.cand.data_ptr(), self.log.data_ptr(), self.log_capacity, st),
+                "mpc_episode_exchange_step2")
+            if events:
+                events[1].record()
+                events = None
+            main = torch.cuda.current_stream()
+            self._comm.wait_stream(main)          # after this launch (its candidate)
+            with torch.cuda.stream(self._comm):
+                gather_into(self._gathered, self.cand, self.group)
+                native.check(L.mpc_episode_exchange_mark(
+                    self.state.data_ptr(), epoch,
+                    ctypes.c_void_p(self._comm.cuda_stream)), "mpc_episode_exchange_mark")
+            self._pending = self._gathered
+            self._pend_epoch = epoch
         if events:
             events[1].record()
         if pend is not None:
@@ -388,6 +425,8 @@ class DeviceEpisode:
                 self.local.data_ptr(), ctypes.byref(self.cfg), self.log.data_ptr(),
                 self.log_capacity, st), "mpc_episode_finalize")
         else:
+            if self.overlap:                      # the last collective, then its step
+                torch.cuda.current_stream().wait_stream(self._comm)
             native.check(L.mpc_episode_exchange_flush(
                 ctypes.byref(self.cfg), self.state.data_ptr(), self._integ, pend.data_ptr(),
                 self.world, self.winner.data_ptr(), self.log.data_ptr(), self.log_capacity, st),

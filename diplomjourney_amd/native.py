@@ -39,6 +39,7 @@ EXPORTS = (
     "mpc_fulltree_workspace_bytes", "mpc_fulltree_argmin",
     "mpc_fulltree_batched_workspace_bytes", "mpc_fulltree_argmin_batched",
     "mpc_episodes_state_bytes", "mpc_episodes_reset", "mpc_episodes_run",
+    "mpc_episode_exchange_step2", "mpc_episode_exchange_mark",
 )
 
 HIPCC_FLAGS = [
@@ -174,6 +175,13 @@ def lib():
     L.mpc_episode_exchange_step.argtypes = [ctypes.POINTER(MpcEpisodeConfig), _P, ctypes.c_uint32,
                                             _P, _P, _I64, _I32, _I64, _I32, _P, ctypes.c_size_t,
                                             _P, _I32, _P, _P, _P, _I32, _P]
+    if not (_LIB_OVERRIDE and not hasattr(L, "mpc_episode_exchange_step2")):
+        L.mpc_episode_exchange_step2.restype = ctypes.c_int
+        L.mpc_episode_exchange_step2.argtypes = [
+            ctypes.POINTER(MpcEpisodeConfig), _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _I64,
+            _I32, _I64, _I32, _P, ctypes.c_size_t, _P, _I32, _P, _P, _P, _I32, _P]
+        L.mpc_episode_exchange_mark.restype = ctypes.c_int
+        L.mpc_episode_exchange_mark.argtypes = [_P, ctypes.c_uint32, _P]
     L.mpc_episode_exchange_flush.restype = ctypes.c_int
     L.mpc_episode_exchange_flush.argtypes = [ctypes.POINTER(MpcEpisodeConfig), _P, _I32, _P, _I32,
                                              _P, _P, _I32, _P]
@@ -187,12 +195,13 @@ def lib():
     L.mpc_episode_rollout.restype = ctypes.c_int
     L.mpc_episode_rollout.argtypes = [_P, _P, _P, _I64, _I32, _I64, _I32, _P, ctypes.c_size_t,
                                       _P, ctypes.POINTER(MpcEpisodeConfig), _P, _I32, _P]
-    L.mpc_episodes_state_bytes.restype = ctypes.c_size_t
-    L.mpc_episodes_state_bytes.argtypes = [_I32]
-    L.mpc_episodes_reset.restype = ctypes.c_int
-    L.mpc_episodes_reset.argtypes = [_P, _I32, _P, _P]
-    L.mpc_episodes_run.restype = ctypes.c_int
-    L.mpc_episodes_run.argtypes = [_P, _I32, _I32, _I32, _I32, _P, _I32, _P, _P]
+    if not (_LIB_OVERRIDE and not hasattr(L, "mpc_episodes_run")):   # (older A/B builds)
+        L.mpc_episodes_state_bytes.restype = ctypes.c_size_t
+        L.mpc_episodes_state_bytes.argtypes = [_I32]
+        L.mpc_episodes_reset.restype = ctypes.c_int
+        L.mpc_episodes_reset.argtypes = [_P, _I32, _P, _P]
+        L.mpc_episodes_run.restype = ctypes.c_int
+        L.mpc_episodes_run.argtypes = [_P, _I32, _I32, _I32, _I32, _P, _I32, _P, _P]
     _lib = L
     return L
 

@@ -344,6 +344,26 @@ int mpc_episode_exchange_step(const mpc_episode_config_t* cfg, void* state, uint
                               size_t ws_bytes, const mpc_candidate_t* gathered,
                               int32_t n_gathered, mpc_result_t* out_prev, mpc_candidate_t* local,
                               mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
+/* The exchange step with the collective OFF the launch's critical path: the
+ * all_gather of step k runs on another stream beside launch k+1 (it waits on
+ * an event recorded after launch k) and is followed there by
+ * mpc_episode_exchange_mark(state, epoch of step k); launch k+1 is enqueued
+ * with wait_tag = that epoch and needs no stream edge to the collective —
+ * only its block 0 waits (bounded; chain error 4 on a timeout) for the mark,
+ * then reads the gathered candidates (at most 32 ranks) coherently.  The
+ * other blocks roll out step k+1 meanwhile.  The collective's kernel must be
+ * able to run beside the launch: on a GPU shared this way, give the launch's
+ * stream a CU mask that leaves CUs free for it.  wait_tag 0
+ * = mpc_episode_exchange_step (the gathered array already final on the
+ * launch's stream). */
+int mpc_episode_exchange_step2(const mpc_episode_config_t* cfg, void* state, uint32_t epoch,
+                               uint32_t wait_tag, const double* v_sc, const double* beta_sc,
+                               int64_t n_cand, int32_t n_steps, int64_t index_base,
+                               int32_t integrator, void* ws, size_t ws_bytes,
+                               const mpc_candidate_t* gathered, int32_t n_gathered,
+                               mpc_result_t* out_prev, mpc_candidate_t* local,
+                               mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
+int mpc_episode_exchange_mark(void* state, uint32_t tag, mpc_stream_t stream);
 int mpc_episode_exchange_flush(const mpc_episode_config_t* cfg, void* state, int32_t integrator,
                                const mpc_candidate_t* gathered, int32_t n_gathered,
                                mpc_result_t* out, mpc_episode_log_t* log, int32_t log_capacity,
@@ -385,7 +405,9 @@ int mpc_episode_generate_step(const mpc_episode_config_t* cfg, void* state, int6
 /* Nonzero if a chained step went wrong: 1 = a chained step's wait for the
  * published constants timed out (the launch then ran on stale constants);
  * 2 = cfg's wheelbase form disagreed with the state's; 3 = an exchange step's
- * collection of its block records timed out (`local` then holds none).
+ * collection of its block records timed out (`local` then holds none); 4 = an
+ * overlapped exchange step's wait for the gathered candidates' mark timed out
+ * (the step was not completed: the episode kept its pose).
  * Reads the device state (syncs). */
 int mpc_episode_chain_error(const void* state, int32_t* error, mpc_stream_t stream);
 

@@ -16,7 +16,7 @@ HEADER = native.HEADER
 def _declared():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return set(re.findall(r"\b(mpc_[a-z_]+)\s*\(", text))
+    return set(re.findall(r"\b(mpc_[a-z_0-9]+)\s*\(", text))
 
 
 @pytest.fixture(scope="module")

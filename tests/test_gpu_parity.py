@@ -275,6 +275,47 @@ def test_chained_config_c_events_and_restart_vs_oracle(engine, oracle):
             assert gap < 1e-13, (i, rec.index, ref.index, gap)
 
 
+@pytest.mark.parametrize("integ", ["qk21", "rect+cum"])
+def test_near_tie_candidates_vs_oracle(engine, oracle, integ):
+    """Near ties below the two arithmetics' noise (the device's
+    steering tangent starts from the non-IEEE v_rcp_f64 estimate): 4096
+    candidates whose steering angles climb one ulp at a time from the same
+    control (costs within ~1e-15 of each other), in 4 groups, each followed
+    by exact duplicates of its first candidate.  The chosen index equals the
+    oracle's (reference arithmetic, glibc trig) or, only where the oracle's
+    own costs of the two differ by < 1e-13 relative, another member of the
+    near tie; an exact duplicate never beats the lowest index."""
+    from diplomjourney_amd.abi import make_problem
+    n, ns = 4096, 10
+    beta = np.empty(n)
+    b0 = 0.31
+    for g in range(4):
+        blk = np.arange(1024)
+        base = np.nextafter(b0, 1.0) if g else b0
+        vals = [base]
+        for _ in range(767):
+            vals.append(np.nextafter(vals[-1], 1.0))
+        vals += [vals[0]] * 256                      # exact duplicates of the group's first
+        beta[g * 1024 + blk] = vals
+        b0 = vals[766]
+    vh = np.full((ns, n), 0.55)
+    bh = np.tile(beta, (ns, 1))
+    v = torch.from_numpy(vh).cuda()
+    b = torch.from_numpy(bh).cuda()
+    prob = make_problem(0.2, -0.1, 0.4, 2, 3, 0, 0, 0.5, 0.35, 0.4)
+    engine.rollout_argmin(prob, v, b, incumbent=INC_MAX, integrator=integ)
+    got = engine.fetch()
+    ref, costs, _ = oracle.rollout_argmin(prob, vh, bh, incumbent=INC_MAX,
+                                          integ="qk21" if integ == "qk21" else "rect",
+                                          want_costs=True)
+    _same_choice(got, ref, costs)
+    # an exact duplicate of an earlier candidate is never the winner
+    first = {}
+    for k in range(n):
+        first.setdefault(bh[0, k], k)
+    assert first[bh[0, got.index]] == got.index
+
+
 def test_sharded_exchange_equals_single_launch(engine):
     """Config D emulated on one device: 8 contiguous shards (index_base) +
     the device all-reduce(min+index) selection == one launch over all."""
@@ -878,9 +919,12 @@ def test_chained_wheelbase_mismatch_is_flagged(engine, ns):
     assert ep.chain_error() == 2
 
 
-@pytest.mark.parametrize("wheelbase,n,cap", [(0.5, 40_000, 6), (0.45, 40_000, 6),
-                                             (0.5, 1_000_000, 1)])
-def test_chained_exchange_path_and_graph_capture(engine, wheelbase, n, cap):
+@pytest.mark.parametrize("wheelbase,n,cap,overlap", [(0.5, 40_000, 6, False),
+                                                     (0.45, 40_000, 6, False),
+                                                     (0.5, 1_000_000, 1, False),
+                                                     (0.5, 40_000, 6, True),
+                                                     (0.5, 1_000_000, 3, True)])
+def test_chained_exchange_path_and_graph_capture(engine, wheelbase, n, cap, overlap):
     """The chained multi-GPU step (launch: rollout of step k + selection over
     step k-1's gathered winners; then step k's local finalize and the RCCL
     all_gather) over a 1-rank nccl group, eager and graph-captured, logs the
@@ -910,7 +954,7 @@ def test_chained_exchange_path_and_graph_capture(engine, wheelbase, n, cap):
                                 world_size=1, device_id=torch.device("cuda", 0))
     try:
         ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64,
-                           exchange=True, chain=True, L=wheelbase)
+                           exchange=True, chain=True, L=wheelbase, overlap=overlap)
         for i in range(half):
             ep.step(controls=pool[i])
         ep.flush()
@@ -928,6 +972,54 @@ def test_chained_exchange_path_and_graph_capture(engine, wheelbase, n, cap):
         assert _episode_log(ep) == want
         assert ep.chain_error() == 0
     finally:
+        if own:
+            dist.destroy_process_group()
+
+
+def test_overlapped_exchange_with_a_late_collective(engine):
+    """The overlapped exchange step (mpc_episode_exchange_step2): the
+    all_gather of step k runs on a side stream beside launch k+1, whose block
+    0 waits for the device-side mark.  Here every collective is held back ~1 ms
+    (a spinning kernel in front of it on the side stream), so each launch's
+    block 0 waits for the mark while its tiles stream: the episode still logs
+    exactly the single-GPU chained episode, chain_error 0."""
+    import torch.distributed as dist
+    from diplomjourney_amd import distributed as D
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.episode import DeviceEpisode
+    n, ns, steps = 200_000, 10, 10
+    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
+    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
+    pool = [engine.sample_controls(V, B, n, ns, 1300 + i) for i in range(steps)]
+    ref = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64, chain=True)
+    for i in range(steps):
+        ref.step(controls=pool[i])
+    want = _episode_log(ref)
+    own = not dist.is_initialized()
+    if own:
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                world_size=1, device_id=torch.device("cuda", 0))
+    orig = D.gather_into
+
+    def late(out, local, group=None):
+        torch.cuda._sleep(2_000_000)          # ~1 ms on the side stream, before the collective
+        return orig(out, local, group)
+    try:
+        import diplomjourney_amd.episode as E
+        E.gather_into = late
+        ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64,
+                           exchange=True, chain=True, overlap=True)
+        for i in range(steps):
+            ep.step(controls=pool[i])
+        ep.flush()
+        assert _episode_log(ep) == want
+        assert ep.chain_error() == 0
+    finally:
+        E.gather_into = orig
         if own:
             dist.destroy_process_group()
 
