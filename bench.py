@@ -425,10 +425,15 @@ def main():
     if args.workload == "G":
         return bench_episodes(args, wl, eng, rank, world, cpu)
 
-    from diplomjourney_amd.episode import DeviceEpisode, Episode, percentile
+    from diplomjourney_amd.episode import DeviceEpisode, Episode, cu_reserved_stream, percentile
     n_total = (args.candidates_per_gpu or wl["per_gpu"]) * world
     n_steps = wl["n_steps"]
     exchange = world > 1 or args.exchange
+    overlap = args.overlap_exchange and exchange and not args.host_loop
+    if overlap:
+        # the steps' launch stream leaves one CU per XCD to the collective that
+        # runs beside each launch (RCCL's kernel never fits beside a full CU)
+        torch.cuda.set_stream(cu_reserved_stream(device, 1))
     # one GPU: the K steps are one HIP graph; with the exchange the RCCL
     # all_gather is captured into the same graph (gloo stages through the
     # host and cannot be captured)
@@ -444,7 +449,7 @@ def main():
                            exchange=exchange, split=not args.fused,
                            chain=not args.no_chain and args.integrator == "rect+cum",
                            generate=inputs == "generated",
-                           overlap=args.overlap_exchange and exchange)
+                           overlap=overlap)
     pool = make_pool(eng, ep, n_steps, args.steps) if inputs == "resident" else None
     rollout_ms = None
     # the launch that carries the step: the chained kernel (rollout of step k +
@@ -544,7 +549,11 @@ def main():
                                       "one launch" + (" (selection over the gathered candidates "
                                                       "of step k-1; the launch also collects "
                                                       "this rank's candidate of step k), then "
-                                                      "the all_gather" if exchange else ""))
+                                                      "the all_gather" if exchange else "")
+                                      + (" on a side stream beside the next launch, whose "
+                                         "block 0 waits for its device-side mark; launches on "
+                                         "a CU-masked stream (1 CU per XCD left to the "
+                                         "collective)" if overlap else ""))
                                      if chain_step
                                      else "rollout, then selection" + (
                                          " + all_gather + advance" if exchange else "")),

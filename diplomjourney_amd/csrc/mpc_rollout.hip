@@ -5,6 +5,7 @@
 //
 // HBM traffic of k_rollout_argmin: 16 B per candidate-step read once
 // (v, beta fp64 SoA), 16 B per block written.  See DESIGN.md for the roofline.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -642,6 +643,34 @@ int mpc_episode_exchange_step2(const mpc_episode_config_t* cfg, void* state, uin
   else
     launch(std::false_type{});
   return last_hip_status();
+}
+
+int mpc_stream_create_cu_reserved(int32_t reserved_per_xcd, mpc_stream_t* stream) {
+  if (!stream || reserved_per_xcd < 0 || reserved_per_xcd > 8) return MPC_ERR_ARG;
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      ncu < 16)
+    return MPC_ERR_HIP;
+  // Logical CU i of a stream's CU mask sits on XCD i % 8: bits 0-7 are CU 0
+  // of XCDs 0-7 (measured, tools/micro/cumask.hip), so clearing the first
+  // 8 * r bits leaves r CUs of every XCD to other streams.
+  uint32_t mask[16];
+  const int words = (ncu + 31) / 32;
+  if (words > 16) return MPC_ERR_UNSUPPORTED;
+  for (int w = 0; w < words; ++w) mask[w] = 0xffffffffu;
+  for (int b = 0; b < 8 * reserved_per_xcd; ++b) mask[b / 32] &= ~(1u << (b % 32));
+  hipStream_t st = nullptr;
+  if (hipExtStreamCreateWithCUMask(&st, static_cast<uint32_t>(words), mask) != hipSuccess)
+    return MPC_ERR_HIP;
+  *stream = reinterpret_cast<mpc_stream_t>(st);
+  return MPC_OK;
+}
+
+int mpc_stream_destroy(mpc_stream_t stream) {
+  if (!stream) return MPC_ERR_ARG;
+  return hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)) == hipSuccess ? MPC_OK
+                                                                               : MPC_ERR_HIP;
 }
 
 int mpc_episode_exchange_mark(void* state, uint32_t tag, mpc_stream_t stream) {

@@ -639,6 +639,20 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+def cu_reserved_stream(device, reserved_per_xcd=1):
+    """A torch stream whose kernels (and hipGraphs replayed on it) leave
+    `reserved_per_xcd` CUs of every XCD free (mpc_stream_create_cu_reserved):
+    the launch stream of the overlapped exchange (DeviceEpisode(overlap=True)),
+    so that the collective running beside a chained launch always finds CUs.
+    Lives as long as the process."""
+    lib = native.lib()
+    p = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        native.check(lib.mpc_stream_create_cu_reserved(int(reserved_per_xcd), ctypes.byref(p)),
+                     "mpc_stream_create_cu_reserved")
+    return torch.cuda.ExternalStream(p.value, device=device)
+
+
 def tree_episode_config(start, max_calls=None):
     """mpc_episode_config_t of one run_math_model.py episode (:231-280) whose
     MPC step is math_model_tree.py's tree expansion (SURVEY Fact 2): start =

@@ -40,6 +40,7 @@ EXPORTS = (
     "mpc_fulltree_batched_workspace_bytes", "mpc_fulltree_argmin_batched",
     "mpc_episodes_state_bytes", "mpc_episodes_reset", "mpc_episodes_run",
     "mpc_episode_exchange_step2", "mpc_episode_exchange_mark",
+    "mpc_stream_create_cu_reserved", "mpc_stream_destroy",
 )
 
 HIPCC_FLAGS = [
@@ -182,6 +183,10 @@ def lib():
             _I32, _I64, _I32, _P, ctypes.c_size_t, _P, _I32, _P, _P, _P, _I32, _P]
         L.mpc_episode_exchange_mark.restype = ctypes.c_int
         L.mpc_episode_exchange_mark.argtypes = [_P, ctypes.c_uint32, _P]
+        L.mpc_stream_create_cu_reserved.restype = ctypes.c_int
+        L.mpc_stream_create_cu_reserved.argtypes = [_I32, ctypes.POINTER(_P)]
+        L.mpc_stream_destroy.restype = ctypes.c_int
+        L.mpc_stream_destroy.argtypes = [_P]
     L.mpc_episode_exchange_flush.restype = ctypes.c_int
     L.mpc_episode_exchange_flush.argtypes = [ctypes.POINTER(MpcEpisodeConfig), _P, _I32, _P, _I32,
                                              _P, _P, _I32, _P]

@@ -364,6 +364,14 @@ int mpc_episode_exchange_step2(const mpc_episode_config_t* cfg, void* state, uin
                                mpc_result_t* out_prev, mpc_candidate_t* local,
                                mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
 int mpc_episode_exchange_mark(void* state, uint32_t tag, mpc_stream_t stream);
+/* A stream whose kernels leave `reserved_per_xcd` CUs of every XCD (0-8)
+ * free for other streams (hipExtStreamCreateWithCUMask): launch the
+ * overlapped exchange steps on it, so the collective's kernel (RCCL's needs
+ * ~280 registers per wave, which never fit beside a chained launch that
+ * fills a CU) always finds CUs.  The mask is a property of the stream a
+ * kernel or a replayed hipGraph is launched on. */
+int mpc_stream_create_cu_reserved(int32_t reserved_per_xcd, mpc_stream_t* stream);
+int mpc_stream_destroy(mpc_stream_t stream);
 int mpc_episode_exchange_flush(const mpc_episode_config_t* cfg, void* state, int32_t integrator,
                                const mpc_candidate_t* gathered, int32_t n_gathered,
                                mpc_result_t* out, mpc_episode_log_t* log, int32_t log_capacity,
