@@ -94,6 +94,7 @@ __global__ __launch_bounds__(kBlock) void k_ft_controls(Consts K, const double* 
 }
 
 constexpr int kFtChunk = 256;  // k2 per wave-item
+constexpr int kFtWaves = 7;    // launch bound (waves per SIMD): <= 72 VGPRs, no scratch (8 spills)
 
 template <int INTEG, bool ROT>
 __device__ __forceinline__ void ft_leaves_body(const Consts& K, double atan_t,
@@ -138,7 +139,7 @@ __device__ __forceinline__ void ft_leaves_body(const Consts& K, double atan_t,
 }
 
 template <int INTEG, bool ROT>
-__global__ __launch_bounds__(kBlock) void k_ft_leaves(Consts K, double atan_t,
+__global__ __launch_bounds__(kBlock, kFtWaves) void k_ft_leaves(Consts K, double atan_t,
                                                       const FtCtl* __restrict__ ctl,
                                                       const uint32_t* __restrict__ no_rot,
                                                       int64_t s1, int64_t item_lo,
@@ -235,7 +236,7 @@ __global__ void k_ft_robots(const mpc_fulltree_problem_t* __restrict__ probs, in
 }
 
 template <int INTEG, bool ROT>
-__global__ __launch_bounds__(kBlock) void k_ft_leaves_batched(
+__global__ __launch_bounds__(kBlock, kFtWaves) void k_ft_leaves_batched(
     const FtRobot* __restrict__ robots, const FtCtl* __restrict__ ctl,
     const uint32_t* __restrict__ no_rot, int64_t s1, Rec* __restrict__ part) {
   const int r = blockIdx.y;

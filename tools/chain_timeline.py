@@ -73,15 +73,16 @@ def build():
     ])
     t = lambda q: f"if (threadIdx.x == 0) {STAMP.format(slot=f'8 * blockIdx.x + {q}')};"   # noqa: E731
     patch(os.path.join(cs, "mpc_episode.h"), [
-        ("  L.status = status;\n  if (ended) episode_restart(c, *S);\n",
-         f"  L.status = status;\n  {b0(6)}\n  if (ended) episode_restart(c, *S);\n"),
+        ("  L.status = status;\n  if (ended) {\n",
+         f"  L.status = status;\n  {b0(6)}\n  if (ended) {{\n"),
         ("  if (blockIdx.x == 0) {\n    if (has_prev) {\n",
          f"  if (blockIdx.x == 0) {{\n    {t(0)}\n    if (has_prev) {{\n"),
-        ("  constexpr int CPL = 2;\n  __shared__ uint32_t s_w[kPubWords], s_tag[kPubWords];\n",
-         f"  {t(0)}\n  constexpr int CPL = 2;\n  __shared__ uint32_t s_w[kPubWords], s_tag[kPubWords];\n"),
+        ("  constexpr int CPL = 2;\n  __shared__ __attribute__((aligned(16))) uint32_t s_w[kPubWords];\n",
+         f"  {t(0)}\n  constexpr int CPL = 2;\n  __shared__ __attribute__((aligned(16))) uint32_t s_w[kPubWords];\n"),
         ("      if (threadIdx.x == 0) s_final = fin;\n    }\n    __syncthreads();\n",
          f"      if (threadIdx.x == 0) s_final = fin;\n    }}\n    __syncthreads();\n    {t(1)}\n"),
-        ("    K = consts_from_words(s_w);\n  };\n", f"    K = consts_from_words(s_w);\n    {t(2)}\n  }};\n"),
+        ("S->chain_error = 1u;\n      }\n      __syncthreads();\n    }\n  };\n",
+         f"S->chain_error = 1u;\n      }}\n      __syncthreads();\n    }}\n    {t(2)}\n  }};\n"),
         ("    else\n      part[blockIdx.x - 1] = Rec{best_k, best_i};\n  }\n}\n",
          "    else\n      part[blockIdx.x - 1] = Rec{best_k, best_i};\n"
          f"    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    {t(3)}\n  }}\n}}\n"),
