@@ -437,7 +437,9 @@ def main():
     # one GPU: the K steps are one HIP graph; with the exchange the RCCL
     # all_gather is captured into the same graph (gloo stages through the
     # host and cannot be captured)
-    use_graph = (not args.host_loop and not args.no_graph
+    # (the overlapped exchange launches eagerly: a replayed graph's parallel
+    # branches lose the launch stream's CU mask)
+    use_graph = (not args.host_loop and not args.no_graph and not overlap
                  and (not exchange or args.dist_backend == "nccl"))
     inputs = "sampled" if args.host_loop else args.inputs
     if args.host_loop:

@@ -622,7 +622,9 @@ __device__ __forceinline__ void store_tagged_rec(Rec* dst, uint64_t key, int64_t
   const uint64_t tag = rec_tag(epoch);
   const uint64_t w0 = (key & ~0xffffull) | tag;
   const uint64_t w1 = (key << 48) | (ix << 16) | tag;
-  asm volatile("global_store_dwordx4 %0, %1, off sc1"
+  // (s_nop 1: the store must read its data registers before the compiler's
+  // next instruction may overwrite them)
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1"
                :
                : "v"(dst), "v"(u64x2{w0, w1})
                : "memory");
@@ -650,17 +652,17 @@ __device__ void collect_local_candidate(const Rec* __restrict__ part, int n_part
                                         int n_steps, int64_t index_base,
                                         mpc_candidate_t* __restrict__ out, uint32_t* err) {
   static_assert(kMaxBlocks <= 8 * kBlock, "eight records per thread");
-  const Rec* ptr[8];
+  uint32_t off[8];   // byte offsets from the (uniform) record base
   u64x2 r[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int p = threadIdx.x + q * kBlock;
-    ptr[q] = part + (p < n_part ? p : n_part - 1);
+    off[q] = static_cast<uint32_t>(p < n_part ? p : n_part - 1) * sizeof(Rec);
   }
   bool timed_out = false;
   const uint32_t tag = rec_tag(epoch);
   for (uint32_t it = 0;; ++it) {
-    load8_rec_sc1(ptr, r);
+    load8_rec_sc1_sbase(part, off, r);
     bool ok = true;
 #pragma unroll
     for (int q = 0; q < 8; ++q)
@@ -688,7 +690,8 @@ __device__ void collect_local_candidate(const Rec* __restrict__ part, int n_part
         // consumed: untag both halves.  A replayed HIP graph repeats its
         // launches' epochs, so a record left tagged would pass for the
         // replay's own before that launch's tile block stores it.
-        *const_cast<u64x2*>(reinterpret_cast<const u64x2*>(ptr[q])) = u64x2{0ull, 0ull};
+        *const_cast<u64x2*>(reinterpret_cast<const u64x2*>(
+            reinterpret_cast<const char*>(part) + off[q])) = u64x2{0ull, 0ull};
       }
     }
   } else if (threadIdx.x == 0) {
@@ -870,8 +873,9 @@ __device__ __forceinline__ bool chain_read(const EpisodeState* S, uint32_t epoch
 
 // Launch bound of the chained kernel (waves per SIMD).  The one-GPU form fits
 // 6 (80 VGPRs, no scratch; its LDS fits 6 blocks per CU since block 0's
-// re-roll borrows the idle control ring); the exchange form spills at 6 and
-// runs 5 (measured: the 6-wave build's exchange step was ~0.9 us slower).
+// re-roll borrows the idle control ring); the exchange form runs 5 (at 6 it
+// keeps 16 B of scratch; measured, round 4, 3 interleaved pairs: the 6-wave
+// build's exchange launch 36.73 vs 36.31 us, profiles/r04/exchange_waves_ab.txt).
 template <int MODE>
 constexpr int chain_waves() {
   return MODE == kChainFin ? 6 : 5;

@@ -217,6 +217,13 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
       reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p));
 }
 
+// Inline asm whose VMEM instruction takes an SGPR operand (the `saddr` base)
+// must itself provide the wait states the hardware needs between a VALU that
+// writes that SGPR and the VMEM that reads it (5 on CDNA): hipcc's hazard
+// recognizer does not look inside asm statements, and it reloads spilled SGPRs
+// with v_readlane — measured: a v_readlane of the base right before the load,
+// 0 wait states, faulted.  Hence the `s_nop 4` ahead of the first such VMEM in
+// every statement below (the M0 write's own 1-wait-state need is covered too).
 // Both control rows of one step into LDS (v at dst_v, beta at dst_b).  The
 // addresses are SGPR base + 32-bit VGPR offset (the `saddr` form): the row
 // bases gv / gb (step s's rows: wave-uniform) advance per step on the SALU,
@@ -234,7 +241,7 @@ __device__ __forceinline__ void glds_pair(const double* gv, const double* gb, ui
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %4\n\t"
-      "s_nop 0\n\t"
+      "s_nop 4\n\t"
       "global_load_lds_dwordx4 %1, %2" MPC_GLDS_POLICY "\n\t"
       "s_mov_b32 m0, %5\n\t"
       "s_nop 0\n\t"
@@ -252,7 +259,7 @@ __device__ __forceinline__ void glds_refill(const double* gv, const double* gb, 
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %4\n\t"
-      "s_nop 0\n\t"
+      "s_nop 4\n\t"
       "global_load_lds_dwordx4 %1, %2" MPC_GLDS_POLICY "\n\t"
       "s_mov_b32 m0, %5\n\t"
       "s_nop 0\n\t"
@@ -901,6 +908,29 @@ __device__ __forceinline__ void load8_rec_sc1(const Rec* const (&p)[8], u64x2 (&
       : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]),
         "=&v"(r[6]), "=&v"(r[7])
       : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
+      : "memory");
+}
+
+// The same from a wave-uniform base (SGPR pair) and 32-bit byte offsets: one
+// VGPR per address instead of two (block 0 of the chained exchange step polls
+// its records with these, and its register peak is the kernel's).
+__device__ __forceinline__ void load8_rec_sc1_sbase(const Rec* base, const uint32_t (&o)[8],
+                                                    u64x2 (&r)[8]) {
+  asm volatile(
+      "s_nop 4\n\t"   // VALU-written SGPR -> VMEM: see glds_pair
+      "global_load_dwordx4 %0, %8, %16 sc1\n\t"
+      "global_load_dwordx4 %1, %9, %16 sc1\n\t"
+      "global_load_dwordx4 %2, %10, %16 sc1\n\t"
+      "global_load_dwordx4 %3, %11, %16 sc1\n\t"
+      "global_load_dwordx4 %4, %12, %16 sc1\n\t"
+      "global_load_dwordx4 %5, %13, %16 sc1\n\t"
+      "global_load_dwordx4 %6, %14, %16 sc1\n\t"
+      "global_load_dwordx4 %7, %15, %16 sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]),
+        "=&v"(r[6]), "=&v"(r[7])
+      : "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "v"(o[4]), "v"(o[5]), "v"(o[6]), "v"(o[7]),
+        "s"(base)
       : "memory");
 }
 

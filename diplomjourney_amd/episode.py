@@ -380,6 +380,7 @@ class DeviceEpisode:
         else:
             # the same launch, but the collective of the previous step may
             # still be running beside it: block 0 waits for its mark
+            _check_overlap_stream()
             epoch = self._next_epoch()
             native.check(L.mpc_episode_exchange_step2(
                 ctypes.byref(self.cfg), self.state.data_ptr(), epoch,
@@ -639,6 +640,27 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+_CU_RESERVED = set()   # handles of the streams cu_reserved_stream() made
+
+
+def _check_overlap_stream():
+    """An overlapped exchange launch must leave CUs to the collective that runs
+    beside it: a launch larger than one resident round (config C: 1954 blocks,
+    1536 resident) fills every CU with blocks that wait, at the end of their
+    tile, for block 0 — which waits for the collective.  Eager launches must
+    therefore go to a cu_reserved_stream().  Eager only: a replayed hipGraph
+    runs its parallel branches on runtime streams that carry no CU mask
+    (measured: the 1M-candidate graph's launches filled every CU and block 0
+    timed out, chain error 4)."""
+    if torch.cuda.is_current_stream_capturing():
+        raise ValueError("overlapped exchange: eager launches only (a replayed graph's branches "
+                         "lose the launch stream's CU mask)")
+    if torch.cuda.current_stream().cuda_stream in _CU_RESERVED:
+        return
+    raise ValueError("overlapped exchange: launch on a cu_reserved_stream() so the collective "
+                     "beside each launch finds free CUs")
+
+
 def cu_reserved_stream(device, reserved_per_xcd=1):
     """A torch stream whose kernels (and hipGraphs replayed on it) leave
     `reserved_per_xcd` CUs of every XCD free (mpc_stream_create_cu_reserved):
@@ -650,6 +672,8 @@ def cu_reserved_stream(device, reserved_per_xcd=1):
     with torch.cuda.device(device):
         native.check(lib.mpc_stream_create_cu_reserved(int(reserved_per_xcd), ctypes.byref(p)),
                      "mpc_stream_create_cu_reserved")
+    if reserved_per_xcd > 0:
+        _CU_RESERVED.add(p.value)
     return torch.cuda.ExternalStream(p.value, device=device)
 
 

@@ -934,7 +934,7 @@ def test_chained_exchange_path_and_graph_capture(engine, wheelbase, n, cap, over
     record of the last one survives its consumption."""
     import torch.distributed as dist
     from diplomjourney_amd import math_model_tree as mmt
-    from diplomjourney_amd.episode import DeviceEpisode
+    from diplomjourney_amd.episode import DeviceEpisode, cu_reserved_stream
     ns, steps = 10, 12
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
@@ -952,23 +952,41 @@ def test_chained_exchange_path_and_graph_capture(engine, wheelbase, n, cap, over
             port = s.getsockname()[1]
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
                                 world_size=1, device_id=torch.device("cuda", 0))
+    # the overlapped form launches (and replays) on a CU-reserved stream: the
+    # collective beside each launch needs free CUs (1M candidates: the launch
+    # is larger than one resident round)
+    launch = cu_reserved_stream(torch.device("cuda", 0)) if overlap else torch.cuda.current_stream()
     try:
-        ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64,
-                           exchange=True, chain=True, L=wheelbase, overlap=overlap)
-        for i in range(half):
-            ep.step(controls=pool[i])
-        ep.flush()
         torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        n0 = ep.steps_enqueued
-        with torch.cuda.graph(g):
-            for i in range(half, steps):
+        with torch.cuda.stream(launch):
+            ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64,
+                               exchange=True, chain=True, L=wheelbase, overlap=overlap)
+            for i in range(half):
                 ep.step(controls=pool[i])
             ep.flush()
-        ep.steps_enqueued = n0
-        for _ in range(reps):
-            g.replay()
-            ep.steps_enqueued += steps - half
+        torch.cuda.synchronize()
+        if overlap:
+            # eager only: a replayed graph's branches lose the CU mask
+            with pytest.raises(ValueError, match="eager"):
+                with torch.cuda.graph(torch.cuda.CUDAGraph()):
+                    ep.step(controls=pool[half])
+            with torch.cuda.stream(launch):
+                for i in list(range(half, steps)) * reps:
+                    ep.step(controls=pool[i])
+                    if i == steps - 1:
+                        ep.flush()
+        else:
+            g = torch.cuda.CUDAGraph()
+            n0 = ep.steps_enqueued
+            with torch.cuda.graph(g):
+                for i in range(half, steps):
+                    ep.step(controls=pool[i])
+                ep.flush()
+            ep.steps_enqueued = n0
+            for _ in range(reps):
+                g.replay()
+                ep.steps_enqueued += steps - half
+        torch.cuda.synchronize()
         assert _episode_log(ep) == want
         assert ep.chain_error() == 0
     finally:
@@ -986,7 +1004,7 @@ def test_overlapped_exchange_with_a_late_collective(engine):
     import torch.distributed as dist
     from diplomjourney_amd import distributed as D
     from diplomjourney_amd import math_model_tree as mmt
-    from diplomjourney_amd.episode import DeviceEpisode
+    from diplomjourney_amd.episode import DeviceEpisode, cu_reserved_stream
     n, ns, steps = 200_000, 10, 10
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
@@ -1011,11 +1029,14 @@ def test_overlapped_exchange_with_a_late_collective(engine):
     try:
         import diplomjourney_amd.episode as E
         E.gather_into = late
-        ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64,
-                           exchange=True, chain=True, overlap=True)
-        for i in range(steps):
-            ep.step(controls=pool[i])
-        ep.flush()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(cu_reserved_stream(torch.device("cuda", 0))):
+            ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64,
+                               exchange=True, chain=True, overlap=True)
+            for i in range(steps):
+                ep.step(controls=pool[i])
+            ep.flush()
+        torch.cuda.synchronize()
         assert _episode_log(ep) == want
         assert ep.chain_error() == 0
     finally:
