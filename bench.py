@@ -135,6 +135,11 @@ def parse():
                     help="exchange steps: run the all_gather of step k on a side stream beside "
                          "launch k+1, whose block 0 waits for the collective's device-side mark "
                          "(mpc_episode_exchange_step2) instead of the launch waiting for it")
+    ap.add_argument("--exchange-mode", default="p2p", choices=["rccl", "p2p"],
+                    help="chained exchange steps: rccl = one RCCL all_gather of the 536-B "
+                         "candidates per step between the launches; p2p = no collective, each "
+                         "launch's block 0 stores its candidate into every rank's mailbox over "
+                         "xGMI (mpc_episode_p2p_step)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks on fewer GPUs (exchange staged via host)")
     ap.add_argument("--candidates-per-gpu", type=int, default=None,
@@ -430,6 +435,8 @@ def main():
     n_steps = wl["n_steps"]
     exchange = world > 1 or args.exchange
     overlap = args.overlap_exchange and exchange and not args.host_loop
+    p2p = (args.exchange_mode == "p2p" and exchange and not args.host_loop and not overlap
+           and not args.no_chain and args.integrator == "rect+cum" and args.inputs == "resident")
     if overlap:
         # the steps' launch stream leaves one CU per XCD to the collective that
         # runs beside each launch (RCCL's kernel never fits beside a full CU)
@@ -440,7 +447,7 @@ def main():
     # (the overlapped exchange launches eagerly: a replayed graph's parallel
     # branches lose the launch stream's CU mask)
     use_graph = (not args.host_loop and not args.no_graph and not overlap
-                 and (not exchange or args.dist_backend == "nccl"))
+                 and (not exchange or p2p or args.dist_backend == "nccl"))
     inputs = "sampled" if args.host_loop else args.inputs
     if args.host_loop:
         ep = Episode(eng, n_total, n_steps, rank=rank, world=world,
@@ -451,7 +458,8 @@ def main():
                            exchange=exchange, split=not args.fused,
                            chain=not args.no_chain and args.integrator == "rect+cum",
                            generate=inputs == "generated",
-                           overlap=overlap)
+                           overlap=overlap, p2p=p2p)
+        p2p = bool(getattr(ep, "p2p", False))    # (False if its self-test failed)
     pool = make_pool(eng, ep, n_steps, args.steps) if inputs == "resident" else None
     rollout_ms = None
     # the launch that carries the step: the chained kernel (rollout of step k +
@@ -459,7 +467,8 @@ def main():
     # over the gathered candidates and collects this rank's) or the rollout kernel
     chained = not exchange and getattr(ep, "chain", False) and inputs == "resident"
     xchg_chain = exchange and getattr(ep, "chain", False) and inputs == "resident"
-    kernel = ("k_episode_chain" if chained else XCHG_KERNEL if xchg_chain
+    kernel = ("k_episode_chain" if chained else (P2P_KERNEL if p2p else XCHG_KERNEL)
+              if xchg_chain
               else "k_rollout_argmin_stream")
     main_run = run_steps(args, ep, pool, use_graph, world, device)
     use_graph = main_run["graph"]
@@ -545,13 +554,16 @@ def main():
                    "episodes_started": episodes,
                    "episode_loop": "host" if args.host_loop else "device-resident",
                    "launch": (("hipGraph of the K steps" + (" incl. the RCCL all_gather"
-                                                            if exchange else ""))
+                                                            if exchange and not p2p else ""))
                               if use_graph else "eager"),
                    "step_launches": (("chained: rollout of step k + completion of step k-1 in "
                                       "one launch" + (" (selection over the gathered candidates "
                                                       "of step k-1; the launch also collects "
-                                                      "this rank's candidate of step k), then "
-                                                      "the all_gather" if exchange else "")
+                                                      "this rank's candidate of step k), "
+                                                      + ("which block 0 stores into every rank's "
+                                                         "mailbox (peer stores; no collective)"
+                                                         if p2p else "then the all_gather")
+                                                      if exchange else "")
                                       + (" on a side stream beside the next launch, whose "
                                          "block 0 waits for its device-side mark; launches on "
                                          "a CU-masked stream (1 CU per XCD left to the "
@@ -560,7 +572,8 @@ def main():
                                      else "rollout, then selection" + (
                                          " + all_gather + advance" if exchange else "")),
                    "parallelism": f"candidate-sharded x{world}" + (
-                       (", all_gather(536 B candidates)/step" if chain_step
+                       (", 536-B candidates by peer stores/step" if p2p
+                        else ", all_gather(536 B candidates)/step" if chain_step
                         else ", all_gather(808 B)/step") if exchange else "")},
         "p50_ms": main_run["p50_ms"], "p90_ms": main_run["p90_ms"],
         "p50_note": "GPU time per MPC step (HIP events between step starts, eager launches)",
@@ -571,6 +584,9 @@ def main():
                           "controller receives the chosen control (math_model_tree.py:429); "
                           "reference: 0.361 s p50 per predictive_control at N=3, 451 "
                           "candidates (SURVEY §6)"),
+        "exchange": (None if not exchange else getattr(ep, "p2p_status", None)
+                     or ("all_gather (RCCL)" if args.dist_backend == "nccl"
+                         else "all_gather (gloo)")),
         "chain_error": chain_err,
         "kernel_ms": kern_ms, "kernel_in_step_ms": main_run["kernel_in_step_ms"],
         "roofline": (None if inputs == "generated" else
@@ -853,6 +869,9 @@ def exchange_chain_pass(ep, pool, reps=100, warm=200):
 
 # the exchange form of the chained kernel (k_episode_chain<..., kChainXchg, ...>)
 XCHG_KERNEL = "k_episode_chain[exchange]"
+# ... and its P2P form (k_episode_chain<..., kChainP2P, ...>: the one-GPU
+# chain's records + block 0's mailbox exchange)
+P2P_KERNEL = "k_episode_chain[p2p]"
 TRAFFIC_JSON = {"k_rollout_argmin_stream": "r03_traffic_stream.json",
                 "k_episode_chain": "r03_close/traffic_chain.json",
                 XCHG_KERNEL: "r04/traffic_chain_xchg.json"}

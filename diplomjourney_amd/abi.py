@@ -127,6 +127,7 @@ class MpcFulltreeResult(ctypes.Structure):
 
 RESULT_BYTES = ctypes.sizeof(MpcResult)
 CANDIDATE_BYTES = ctypes.sizeof(MpcCandidate)
+IPC_HANDLE_BYTES = 64   # MPC_IPC_HANDLE_BYTES (hipIpcMemHandle_t)
 FT_RESULT_BYTES = ctypes.sizeof(MpcFulltreeResult)
 LOG_BYTES = ctypes.sizeof(MpcEpisodeLog)
 PROGRESS_BYTES = ctypes.sizeof(MpcEpisodesProgress)

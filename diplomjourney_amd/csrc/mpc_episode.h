@@ -801,7 +801,10 @@ __global__ __launch_bounds__(64) void k_episode_advance(mpc_episode_config_t c,
 // carry different epochs and the update that ends a chain (k_finalize's hook,
 // k_episode_advance) clears the tags.  The wait is bounded: if the words
 // never came, chain_error is set instead of hanging the GPU.
-constexpr int kChainFin = 1, kChainXchg = 3;
+// kChainP2P (multi-GPU, no collective): kChainFin's structure (records to
+// part, the next launch's block 0 reduces them) with the per-rank candidates
+// exchanged through the mailboxes by block 0 (p2p_complete).
+constexpr int kChainFin = 1, kChainXchg = 3, kChainP2P = 4;
 
 // LDS dwords (Consts layout) -> wave-uniform Consts, field by field (no
 // memory view of the struct: it stays in SGPRs).
@@ -871,6 +874,230 @@ __device__ __forceinline__ bool chain_read(const EpisodeState* S, uint32_t epoch
   return __ballot(!ok) == 0;
 }
 
+// ---------------------------------------------------------------------------
+// Peer-to-peer exchange (mpc_episode_p2p_step): no collective launch.  Every
+// rank owns a MAILBOX in its HBM (uncached device memory, mpc_mailbox_alloc:
+// each access goes to HBM, so stores a peer GPU makes over xGMI are what this
+// GPU's loads see).  Block 0 of rank q's launch with epoch e+1 — the launch
+// that completes step e — reduces step e's block records (the previous
+// launch's, stream-ordered: plain loads), stores q's candidate into slot e&1,
+// row q, of EVERY rank's mailbox (its own included) and then, behind its
+// stores' completion, the tag e into that mailbox's tag word (slot, q); it
+// then waits for the `world` tags of slot e&1 in its own mailbox, stages the
+// candidates in LDS, clears the tags, selects the global winner and updates
+// the episode.  The tile blocks meanwhile stream step e+1 (its constants are
+// speculated until block 0 publishes them, as in the one-GPU chain): the
+// exchange runs beside the rollout, not between launches.
+// Two slots suffice: rank q writes slot e&1 again only for step e+2, after it
+// has read every rank's step-(e+1) candidate — each of which its writer
+// posted after clearing its own slot-(e&1) tags.  Accesses are 8-B relaxed
+// system-scope atomics (`sc0 sc1`).
+//   layout: MailHdr (the peers' mailbox pointers as mapped in this process,
+//           this rank, the world size), uint64 tag[2][kMailMaxRanks], then
+//           record[2][world] of kMailRecBytes (an mpc_candidate_t, padded)
+constexpr int kMailMaxRanks = kXchgLdsRanks;
+struct MailHdr {
+  uint64_t peers[kMailMaxRanks];
+  int32_t rank, world;
+  uint64_t ping[kMailMaxRanks];   // mpc_mailbox_ping: rank r's ping word
+};
+constexpr size_t kMailHdrBytes = (sizeof(MailHdr) + 255) & ~size_t{255};
+constexpr size_t kMailTagBytes = 2 * kMailMaxRanks * sizeof(uint64_t);
+constexpr size_t kMailRecBytes = (sizeof(mpc_candidate_t) + 63) & ~size_t{63};
+constexpr int kCandWords = static_cast<int>(sizeof(mpc_candidate_t) / 8);
+static_assert(sizeof(mpc_candidate_t) % 8 == 0, "candidates move as 8-B words");
+// Peers' launches are not stream-ordered with this one: a rank may start its
+// step a host-side hiccup later.  ~1 s before chain error 5.
+constexpr uint32_t kP2PSpinLimit = 1u << 24;
+
+__host__ __device__ inline size_t mailbox_bytes(int world) {
+  return kMailHdrBytes + kMailTagBytes + 2 * static_cast<size_t>(world) * kMailRecBytes;
+}
+
+__device__ __forceinline__ uint64_t* mail_tag(void* mb, uint32_t slot, int rank) {
+  return reinterpret_cast<uint64_t*>(static_cast<char*>(mb) + kMailHdrBytes) +
+         slot * kMailMaxRanks + rank;
+}
+
+__device__ __forceinline__ uint64_t* mail_rec(void* mb, uint32_t slot, int rank, int world) {
+  return reinterpret_cast<uint64_t*>(static_cast<char*>(mb) + kMailHdrBytes + kMailTagBytes +
+                                     (static_cast<size_t>(slot) * world + rank) * kMailRecBytes);
+}
+
+// Where block 0 stages candidates: the control ring's LDS after the re-roll's
+// EmitLds (the ring is idle in block 0).
+__device__ __forceinline__ mpc_candidate_t* cand_lds() {
+  return reinterpret_cast<mpc_candidate_t*>(reinterpret_cast<char*>(ring_lds()) +
+                                            ((sizeof(EmitLds) + 15) & ~size_t{15}));
+}
+
+// Block 0, all threads: this rank's best candidate of the previous launch —
+// the lexicographic (cost, local index) minimum of its n_part block records
+// (plain 16-B records of a stream-ordered earlier launch), its global index
+// and its controls — into `out` (LDS).
+__device__ void records_candidate(const Rec* __restrict__ part, int n_part,
+                                  const double* __restrict__ v, const double* __restrict__ b,
+                                  int64_t n_cand, int n_steps, int64_t index_base,
+                                  mpc_candidate_t* out) {
+  constexpr int kPer = static_cast<int>((kMaxBlocks + kBlock - 1) / kBlock);
+  Rec r[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {   // every load issued before any compare
+    const int p = threadIdx.x + q * kBlock;
+    r[q] = p < n_part ? part[p] : Rec{~0ull, INT64_MAX};
+  }
+  uint64_t k = ~0ull;
+  int64_t i = INT64_MAX;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q)
+    if (rec_less(r[q].key, r[q].idx, k, i)) {
+      k = r[q].key;
+      i = r[q].idx;
+    }
+  block_argmin(k, i);
+  __shared__ uint64_t s_k;
+  __shared__ int64_t s_i;
+  if (threadIdx.x == 0) {
+    s_k = k;
+    s_i = i;
+  }
+  __syncthreads();
+  k = s_k;
+  i = s_i;
+  const bool valid = k != ~0ull;
+  const int q = threadIdx.x;
+  if (q < MPC_MAX_STEPS) {   // one value per lane
+    out->v[q] = (valid && q < n_steps) ? v[q * n_cand + i] : 0.0;
+    out->beta[q] = (valid && q < n_steps) ? b[q * n_cand + i] : 0.0;
+  }
+  if (q == 0) {
+    out->cost = valid ? key_cost(k) : __builtin_inf();
+    out->index = valid ? index_base + i : -1;
+    out->n_steps = n_steps;
+    out->reserved_ = 0;
+  }
+}
+
+// Block 0, all threads: post this rank's candidate (in LDS) of step `tag` to
+// every rank's mailbox: the record words, every storing wave's wait for its
+// stores, a barrier, then one tag store per rank.
+__device__ void post_candidate(void* mb, int world, uint32_t tag, const mpc_candidate_t* cand) {
+  const uint32_t slot = tag & 1u;
+  const MailHdr* hdr = static_cast<const MailHdr*>(mb);
+  const int rank = hdr->rank;
+  __syncthreads();   // the candidate is complete in LDS
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(cand);
+  for (int q = threadIdx.x; q < world * kCandWords; q += blockDim.x) {
+    const int r = q / kCandWords, w = q - r * kCandWords;
+    void* peer = reinterpret_cast<void*>(hdr->peers[r]);
+    __hip_atomic_store(mail_rec(peer, slot, rank, world) + w, src[w], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // (the tag-clearing stores of the previous wait_mailbox are among the
+  // waited ones: a peer sees this step's candidate only after they completed)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (static_cast<int>(threadIdx.x) < world)
+    __hip_atomic_store(mail_tag(reinterpret_cast<void*>(hdr->peers[threadIdx.x]), slot, rank),
+                       static_cast<uint64_t>(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Block 0, all threads: wait (bounded; chain error 5) for every rank's
+// candidate of step `tag` in this rank's mailbox, copy them into LDS
+// (cand_lds) and clear the tags.  Returns the LDS copy, or nullptr on a
+// timeout.
+__device__ const mpc_candidate_t* wait_mailbox(EpisodeState* S, void* mb, uint32_t tag,
+                                               int world) {
+  __shared__ int s_ok;
+  const uint32_t slot = tag & 1u;
+  if (threadIdx.x < 64) {   // wave 0; lane r watches rank r's tag
+    bool seen = static_cast<int>(threadIdx.x) >= world;
+    uint32_t it = 0;
+    for (; it < kP2PSpinLimit; ++it) {
+      if (!seen)
+        seen = static_cast<uint32_t>(__hip_atomic_load(mail_tag(mb, slot, threadIdx.x),
+                                                       __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_SYSTEM)) == tag;
+      if (__ballot(!seen) == 0) break;   // (uniform over the wave)
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (threadIdx.x == 0) {
+      s_ok = it < kP2PSpinLimit;
+      if (it >= kP2PSpinLimit) S->chain_error = 5u;
+    }
+  }
+  __syncthreads();
+  if (!s_ok) return nullptr;
+  mpc_candidate_t* dst = cand_lds();
+  for (int q = threadIdx.x; q < world * kCandWords; q += blockDim.x) {
+    const int r = q / kCandWords, w = q - r * kCandWords;
+    reinterpret_cast<uint64_t*>(dst)[q] = __hip_atomic_load(
+        mail_rec(mb, slot, r, world) + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();   // every load has returned (its value is in LDS)
+  if (static_cast<int>(threadIdx.x) < world)
+    __hip_atomic_store(mail_tag(mb, slot, threadIdx.x), uint64_t{0}, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  return dst;
+}
+
+// Block 0 of a P2P launch (and the flush): complete step `tag` = prev: this
+// rank's candidate from the previous launch's records, posted; the world
+// candidates awaited; the global winner re-rolled into out_prev and the
+// episode updated, publishing `publish_epoch` (0: end of the chain).
+template <int INTEG, int ROT>
+__device__ void p2p_complete(const mpc_episode_config_t& c, EpisodeState* S, void* mb, int world,
+                             uint32_t prev, const Rec* __restrict__ part_prev, int n_part_prev,
+                             const double* __restrict__ v_prev, const double* __restrict__ b_prev,
+                             int64_t n_cand, int n_steps, int64_t index_base,
+                             mpc_result_t* __restrict__ out_prev,
+                             mpc_episode_log_t* __restrict__ log, int cap, uint32_t publish_epoch) {
+  mpc_candidate_t* lc = cand_lds();
+  records_candidate(part_prev, n_part_prev, v_prev, b_prev, n_cand, n_steps, index_base, lc);
+  post_candidate(mb, world, prev, lc);
+  const mpc_candidate_t* g = wait_mailbox(S, mb, prev, world);
+  if (g) {
+    advance_from_candidates<INTEG, ROT>(c, S, g, world, out_prev, log, cap, publish_epoch,
+                                        ring_lds());
+  } else if (publish_epoch) {   // timed out (error 5): publish the unchanged head
+    chain_publish(S, publish_epoch);
+  } else if (threadIdx.x < kPubWords) {   // ... or still end the chain
+    __hip_atomic_store(&S->chain_pub[threadIdx.x], uint64_t{0}, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// The mailboxes' self-test (mpc_mailbox_ping): lane r stores `tag` into
+// rank r's ping word for this rank, then every lane waits (~0.1 s at most)
+// for its rank's word in this mailbox; ok[0] = 1 if all `world` arrived.
+__global__ __launch_bounds__(64) void k_mailbox_ping(void* mb, uint32_t tag, int32_t* ok) {
+  MailHdr* hdr = static_cast<MailHdr*>(mb);
+  const int world = hdr->world, rank = hdr->rank;
+  const int r = threadIdx.x;
+  if (r < world)
+    __hip_atomic_store(&static_cast<MailHdr*>(reinterpret_cast<void*>(hdr->peers[r]))->ping[rank],
+                       static_cast<uint64_t>(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  bool seen = r >= world;
+  for (uint32_t it = 0; it < kChainSpinLimit && __ballot(!seen) != 0; ++it) {
+    if (!seen)
+      seen = __hip_atomic_load(&hdr->ping[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ==
+             static_cast<uint64_t>(tag);
+    __builtin_amdgcn_s_sleep(8);
+  }
+  const bool all = __ballot(!seen) == 0;
+  if (r == 0) ok[0] = all ? 1 : 0;
+}
+
+template <int INTEG, int ROT>
+__global__ __launch_bounds__(kBlock) void k_episode_p2p_flush(
+    mpc_episode_config_t c, EpisodeState* __restrict__ S, void* mailbox, uint32_t tag, int world,
+    const Rec* __restrict__ part, int n_part, const double* __restrict__ v,
+    const double* __restrict__ b, int64_t n_cand, int n_steps, int64_t index_base,
+    mpc_result_t* __restrict__ out, mpc_episode_log_t* __restrict__ log, int cap) {
+  p2p_complete<INTEG, ROT>(c, S, mailbox, world, tag, part, n_part, v, b, n_cand, n_steps,
+                           index_base, out, log, cap, 0u);
+}
+
 // Launch bound of the chained kernel (waves per SIMD).  The one-GPU form fits
 // 6 (80 VGPRs, no scratch; its LDS fits 6 blocks per CU since block 0's
 // re-roll borrows the idle control ring); the exchange form runs 5 (at 6 it
@@ -878,7 +1105,7 @@ __device__ __forceinline__ bool chain_read(const EpisodeState* S, uint32_t epoch
 // build's exchange launch 36.73 vs 36.31 us, profiles/r04/exchange_waves_ab.txt).
 template <int MODE>
 constexpr int chain_waves() {
-  return MODE == kChainFin ? 6 : 5;
+  return MODE == kChainXchg ? 5 : 6;
 }
 
 // PL2 (wheelbase a power of two) is a template parameter, not a runtime
@@ -898,7 +1125,15 @@ __global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
     if (has_prev) {
       // the completion of step k-1 publishes step k's constants itself, from
       // its LDS copy of the updated head (store_update)
-      if constexpr (MODE == kChainFin) {
+      if constexpr (MODE == kChainP2P) {
+        // the previous launch's records -> this rank's candidate, posted to
+        // every mailbox; the world's awaited; selection and update.
+        // (`gathered` carries the mailbox, n_gathered the world size, wait_tag
+        // the previous step's epoch)
+        p2p_complete<INTEG, ROT>(ecfg, S, const_cast<mpc_candidate_t*>(gathered), n_gathered,
+                                 wait_tag, part_prev, n_part_prev, v_prev, b_prev, n_cand,
+                                 n_steps, index_base, out_prev, log, cap, epoch);
+      } else if constexpr (MODE == kChainFin) {
         const Consts Kp = S->h.K;
         const EpisodeHook hook{&S->h, log, cap, S->chain_pub, kPubWords, epoch};
         // (block 0 never fills the control ring: its LDS holds the re-roll)
@@ -908,7 +1143,9 @@ __global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
                                                         ring_lds());
       } else {
         // overlapped exchange: the gathered candidates come from a collective
-        // that ran beside this launch — wait for its mark, stage them in LDS
+        // that ran beside this launch — wait for its mark, stage them in LDS.
+        // P2P: wait for them in this rank's mailbox (`gathered` carries it,
+        // n_gathered the world size, wait_tag the previous step's epoch).
         const mpc_candidate_t* g =
             wait_tag ? wait_gathered(S, wait_tag, gathered, n_gathered) : gathered;
         if (g)

@@ -694,6 +694,156 @@ int mpc_episode_exchange_flush(const mpc_episode_config_t* cfg, void* state, int
   return last_hip_status();
 }
 
+// ------------------------ peer-to-peer exchange ------------------------------
+size_t mpc_mailbox_bytes(int32_t world) {
+  return world < 1 || world > kMailMaxRanks ? 0 : mailbox_bytes(world);
+}
+
+int mpc_mailbox_alloc(int32_t world, int32_t uncached, void** mailbox) {
+  const size_t n = mpc_mailbox_bytes(world);
+  if (!n || !mailbox) return MPC_ERR_ARG;
+  *mailbox = nullptr;
+  void* p = nullptr;
+  if ((uncached ? hipExtMallocWithFlags(&p, n, hipDeviceMallocUncached) : hipMalloc(&p, n)) !=
+      hipSuccess)
+    return MPC_ERR_HIP;
+  // zeroed before the caller can hand it out: no peer ever sees a stale tag
+  if (hipMemset(p, 0, n) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    (void)hipFree(p);
+    return MPC_ERR_HIP;
+  }
+  *mailbox = p;
+  return MPC_OK;
+}
+
+int mpc_mailbox_free(void* mailbox) {
+  if (!mailbox) return MPC_ERR_ARG;
+  return hipFree(mailbox) == hipSuccess ? MPC_OK : MPC_ERR_HIP;
+}
+
+int mpc_ipc_handle(void* dev_ptr, void* handle) {
+  static_assert(sizeof(hipIpcMemHandle_t) == MPC_IPC_HANDLE_BYTES, "IPC handle size");
+  if (!dev_ptr || !handle) return MPC_ERR_ARG;
+  hipIpcMemHandle_t h;
+  if (hipIpcGetMemHandle(&h, dev_ptr) != hipSuccess) return MPC_ERR_HIP;
+  memcpy(handle, &h, sizeof(h));
+  return MPC_OK;
+}
+
+int mpc_ipc_open(const void* handle, void** dev_ptr) {
+  if (!handle || !dev_ptr) return MPC_ERR_ARG;
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  *dev_ptr = nullptr;
+  return hipIpcOpenMemHandle(dev_ptr, h, hipIpcMemLazyEnablePeerAccess) == hipSuccess
+             ? MPC_OK
+             : MPC_ERR_HIP;
+}
+
+int mpc_ipc_close(void* dev_ptr) {
+  if (!dev_ptr) return MPC_ERR_ARG;
+  return hipIpcCloseMemHandle(dev_ptr) == hipSuccess ? MPC_OK : MPC_ERR_HIP;
+}
+
+int mpc_peer_enable(int32_t peer_device) {
+  int dev = 0, n = 0, can = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceCount(&n) != hipSuccess) return MPC_ERR_HIP;
+  if (peer_device < 0 || peer_device >= n) return MPC_ERR_ARG;
+  if (peer_device == dev) return MPC_OK;
+  if (hipDeviceCanAccessPeer(&can, dev, peer_device) != hipSuccess || !can)
+    return MPC_ERR_UNSUPPORTED;
+  const hipError_t e = hipDeviceEnablePeerAccess(peer_device, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+  return e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled ? MPC_OK : MPC_ERR_HIP;
+}
+
+int mpc_mailbox_set_peers(void* mailbox, int32_t rank, int32_t world, const void* const* peers) {
+  if (!mailbox || !peers || world < 1 || world > kMailMaxRanks || rank < 0 || rank >= world)
+    return MPC_ERR_ARG;
+  MailHdr h = {};   // (ping words zeroed too: mpc_mailbox_ping before any peer pings)
+  for (int r = 0; r < world; ++r) {
+    if (!peers[r]) return MPC_ERR_ARG;
+    h.peers[r] = reinterpret_cast<uint64_t>(peers[r]);
+  }
+  if (peers[rank] != mailbox) return MPC_ERR_ARG;   // own row: the local mapping
+  h.rank = rank;
+  h.world = world;
+  return hipMemcpy(mailbox, &h, sizeof(h), hipMemcpyHostToDevice) == hipSuccess ? MPC_OK
+                                                                                : MPC_ERR_HIP;
+}
+
+int mpc_mailbox_ping(void* mailbox, uint32_t tag, int32_t* ok, mpc_stream_t stream) {
+  if (!mailbox || !ok || tag == 0) return MPC_ERR_ARG;
+  k_mailbox_ping<<<1, 64, 0, reinterpret_cast<hipStream_t>(stream)>>>(mailbox, tag, ok);
+  return last_hip_status();
+}
+
+int mpc_episode_p2p_step(const mpc_episode_config_t* cfg, void* state, uint32_t epoch,
+                         uint32_t prev_epoch, const double* v_sc, const double* beta_sc,
+                         int64_t n_cand, int32_t n_steps, int64_t index_base, int32_t integrator,
+                         void* ws, const void* ws_prev, size_t ws_bytes, const double* v_prev,
+                         const double* beta_prev, void* mailbox, int32_t world,
+                         mpc_result_t* out_prev, mpc_episode_log_t* log, int32_t log_capacity,
+                         mpc_stream_t stream) {
+  if (check_episode_cfg(cfg) != MPC_OK ||
+      check_episode_arrays(state, v_sc, beta_sc, n_cand, n_steps) != MPC_OK || index_base < 0 ||
+      log_capacity < 0 || epoch == 0 || !mailbox || world < 1 || world > kMailMaxRanks)
+    return MPC_ERR_ARG;
+  if (prev_epoch) {
+    // consecutive steps use the two mailbox slots alternately (epoch & 1)
+    if (((epoch ^ prev_epoch) & 1u) == 0 || !out_prev || !ws_prev || !v_prev || !beta_prev)
+      return MPC_ERR_ARG;
+  }
+  if (mode_ok(integrator) != MPC_OK || !is_cum(integrator) || !wide_ok(v_sc, beta_sc, n_cand) ||
+      (prev_epoch && !wide_ok(v_prev, beta_prev, n_cand)))
+    return MPC_ERR_UNSUPPORTED;
+  if (!ws || ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
+  EpisodeState* S = static_cast<EpisodeState*>(state);
+  int e;
+  const int pl2 = frexp(cfg->L, &e) == 0.5 ? 1 : 0;
+  // block 0 + one block per tile; the previous step's records are as many
+  const int64_t tiles = rollout_grid<kCplWide>(n_cand);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  constexpr int I = MPC_INTEG_RECT;
+  // (the exchange form's argument slots: gathered = this rank's mailbox,
+  // n_gathered = world, wait_tag = the previous step's epoch)
+  auto launch = [&](auto pl2_tag) {
+    constexpr bool P = decltype(pl2_tag)::value;
+    k_episode_chain<I, kRotCum, kChainP2P, P><<<tiles + 1, kBlock, 0, st>>>(
+        S, epoch, v_sc, beta_sc, n_cand, n_steps, static_cast<Rec*>(ws), prev_epoch ? 1 : 0,
+        static_cast<const Rec*>(ws_prev), static_cast<int>(tiles), v_prev, beta_prev,
+        index_base, out_prev, static_cast<const mpc_candidate_t*>(mailbox), world, *cfg, log,
+        log_capacity, prev_epoch);
+  };
+  if (pl2)
+    launch(std::true_type{});
+  else
+    launch(std::false_type{});
+  return last_hip_status();
+}
+
+int mpc_episode_p2p_flush(const mpc_episode_config_t* cfg, void* state, uint32_t last_epoch,
+                          const double* v_last, const double* beta_last, int64_t n_cand,
+                          int32_t n_steps, int64_t index_base, int32_t integrator,
+                          const void* ws_last, size_t ws_bytes, void* mailbox, int32_t world,
+                          mpc_result_t* out, mpc_episode_log_t* log, int32_t log_capacity,
+                          mpc_stream_t stream) {
+  if (check_episode_cfg(cfg) != MPC_OK ||
+      check_episode_arrays(state, v_last, beta_last, n_cand, n_steps) != MPC_OK ||
+      index_base < 0 || !mailbox || last_epoch == 0 || world < 1 || world > kMailMaxRanks ||
+      !out || log_capacity < 0 || !ws_last)
+    return MPC_ERR_ARG;
+  if (mode_ok(integrator) != MPC_OK || !is_cum(integrator) || !wide_ok(v_last, beta_last, n_cand))
+    return MPC_ERR_UNSUPPORTED;
+  if (ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
+  k_episode_p2p_flush<MPC_INTEG_RECT, kRotCum>
+      <<<1, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+          *cfg, static_cast<EpisodeState*>(state), mailbox, last_epoch, world,
+          static_cast<const Rec*>(ws_last), static_cast<int>(rollout_grid<kCplWide>(n_cand)),
+          v_last, beta_last, n_cand, n_steps, index_base, out, log, log_capacity);
+  return last_hip_status();
+}
+
 // ----------------------------- RCCL exchange --------------------------------
 int mpc_comm_unique_id(void* id) {
   const rccl::Api& r = rccl::api();

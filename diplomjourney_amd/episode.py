@@ -25,7 +25,7 @@ import time
 import torch
 
 from . import math_model_tree as mmt
-from .abi import (CANDIDATE_BYTES, LOG_BYTES, MPC_EP_ARRIVED, MPC_EP_BREAK, MPC_EP_EVENT,
+from .abi import (CANDIDATE_BYTES, IPC_HANDLE_BYTES, LOG_BYTES, MPC_EP_ARRIVED, MPC_EP_BREAK, MPC_EP_EVENT,
                   MPC_EP_LIMIT, MPC_EP_STALE, MPC_EP_STUCK, RESULT_BYTES, MpcEpisodeConfig,
                   MpcEpisodeLog, make_problem)
 from .distributed import exchange_winner, gather_bytes, gather_into, gather_results, shard_range
@@ -40,6 +40,8 @@ CHAIN_ERRORS = {
        "candidate dropped out of the global arg-min)",
     4: "an overlapped exchange launch's block 0 timed out waiting for the all_gather's mark "
        "(the collective could not run beside the launch: the step was not completed)",
+    5: "a P2P exchange launch's block 0 timed out waiting for the ranks' candidates in its "
+       "mailbox (a peer did not run the same step: the step was not completed)",
 }
 
 
@@ -249,7 +251,8 @@ class DeviceEpisode:
     def __init__(self, engine, n_cand_total, n_steps, rank=0, world=1, seed=20261015,
                  integrator="rect", group=None, start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3),
                  log_capacity=4096, split=True, exchange=None, chain=False, L=None,
-                 generate=False, max_steps=0, incumbent0=0.0, enumerate=False, overlap=False):
+                 generate=False, max_steps=0, incumbent0=0.0, enumerate=False, overlap=False,
+                 p2p=False, mailbox_uncached=True):
         self.eng = engine
         self.lib = native.lib()
         self.n_total = int(n_cand_total)
@@ -303,6 +306,18 @@ class DeviceEpisode:
             raise ValueError("overlap: at most 32 ranks (gathered candidates staged in LDS)")
         self._gathered = torch.zeros(self.world * CANDIDATE_BYTES, dtype=torch.uint8, device=dev)
         self._comm = torch.cuda.Stream(device=dev) if self.overlap else None
+        # p2p (exchange + chain): no collective — each launch's block 0 stores
+        # its rank's candidate into every rank's mailbox over xGMI and the next
+        # launch's block 0 waits for the world candidates in its own
+        # (mpc_episode_p2p_step); see _p2p_setup
+        self.p2p = bool(p2p)
+        if self.p2p and (self.overlap or not (self.exchange and self.chain)):
+            raise ValueError("p2p: the chained exchange step (exchange=True, chain=True), "
+                             "not overlapped")
+        self._mailbox, self._opened = None, []
+        self.p2p_status = None
+        if self.p2p:
+            self._p2p_setup(dev, bool(mailbox_uncached))
         self._pend_epoch = 0
         # generate: steps without caller controls draw their candidates inside
         # the rollout (mpc_episode_generate_step) instead of sampling them into
@@ -319,6 +334,96 @@ class DeviceEpisode:
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def _p2p_setup(self, dev, uncached):
+        """This rank's mailbox, the ranks' IPC handles exchanged once over the
+        process group, the peers' mailboxes opened and written into this
+        mailbox's header, then a self-test of the mailboxes (mpc_mailbox_ping)
+        on every rank.  If any rank fails any of it, every rank falls back to
+        the all_gather exchange (self.p2p = False; the reason in
+        self.p2p_status)."""
+        L = self.lib
+        if self.world > 32:
+            raise ValueError("p2p: at most 32 ranks")
+        self.p2p_status = "mailbox peer stores"
+        ok = 1
+        h = (ctypes.c_uint8 * IPC_HANDLE_BYTES)()
+        try:
+            mb = ctypes.c_void_p()
+            with torch.cuda.device(dev):
+                native.check(L.mpc_mailbox_alloc(self.world, int(uncached), ctypes.byref(mb)),
+                             "mpc_mailbox_alloc")
+            self._mailbox = mb.value
+            if self.world > 1:
+                native.check(L.mpc_ipc_handle(ctypes.c_void_p(self._mailbox), h),
+                             "mpc_ipc_handle")
+        except RuntimeError as e:
+            ok, self.p2p_status = 0, f"fell back to all_gather: {e}"
+        if self._all_ok(ok, dev):
+            try:
+                ptrs = [0] * self.world
+                ptrs[self.rank] = self._mailbox
+                if self.world > 1:
+                    local = torch.tensor(bytearray(h), dtype=torch.uint8, device=dev)
+                    handles = gather_bytes(local, self.group).cpu().numpy().reshape(self.world, -1)
+                    for r in range(self.world):
+                        if r == self.rank:
+                            continue
+                        p = ctypes.c_void_p()
+                        hr = (ctypes.c_uint8 * IPC_HANDLE_BYTES).from_buffer_copy(
+                            handles[r].tobytes())
+                        native.check(L.mpc_ipc_open(hr, ctypes.byref(p)), "mpc_ipc_open")
+                        self._opened.append(p.value)
+                        ptrs[r] = p.value
+                arr = (ctypes.c_void_p * self.world)(*ptrs)
+                with torch.cuda.device(dev):
+                    native.check(L.mpc_mailbox_set_peers(ctypes.c_void_p(self._mailbox),
+                                                         self.rank, self.world, arr),
+                                 "mpc_mailbox_set_peers")
+            except RuntimeError as e:
+                ok, self.p2p_status = 0, f"fell back to all_gather: {e}"
+        else:
+            ok = 0
+        if self._all_ok(ok, dev):
+            # every rank's header is written (the all_ok above is a barrier)
+            flag = torch.zeros(1, dtype=torch.int32, device=dev)
+            with torch.cuda.device(dev):
+                native.check(L.mpc_mailbox_ping(ctypes.c_void_p(self._mailbox), 0x5A17,
+                                                flag.data_ptr(), self._stream()),
+                             "mpc_mailbox_ping")
+            ok = int(flag.item())
+            if not ok:
+                self.p2p_status = "fell back to all_gather: the mailbox self-test timed out"
+            ok = self._all_ok(ok, dev)
+        else:
+            ok = 0
+        if not ok:
+            if self.p2p_status == "mailbox peer stores":
+                self.p2p_status = "fell back to all_gather: a peer's mailbox setup failed"
+            self.close()
+            self.p2p = False
+        self._prev_epoch = 0
+
+    def _all_ok(self, ok, dev):
+        """min over the ranks of a 0/1 flag (a collective: every rank calls it)."""
+        if self.world == 1:
+            return int(ok)
+        import torch.distributed as dist
+        on_dev = dist.get_backend(self.group) == "nccl"
+        t = torch.tensor([int(ok)], dtype=torch.int32, device=dev if on_dev else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return int(t.item())
+
+    def close(self):
+        """Release the P2P mailbox and the peers' mappings (idempotent)."""
+        L = self.lib
+        for p in self._opened:
+            L.mpc_ipc_close(ctypes.c_void_p(p))
+        self._opened = []
+        if self._mailbox:
+            torch.cuda.synchronize()
+            L.mpc_mailbox_free(ctypes.c_void_p(self._mailbox))
+            self._mailbox = None
 
     def reset(self):
         native.check(self.lib.mpc_episode_reset(ctypes.byref(self.cfg), self.state.data_ptr(),
@@ -362,6 +467,21 @@ class DeviceEpisode:
                 ws_prev.data_ptr(), ws.numel(), pv, pb, self.local.data_ptr(), None, 0,
                 self.log.data_ptr(), self.log_capacity, st), "mpc_episode_chain_step")
             self._pending = (v, b)
+        elif self.p2p:
+            # one launch: rollout of step k; its block 0 completes step k-1 —
+            # this rank's candidate posted to every mailbox over xGMI, the
+            # world's awaited, selection + update (no collective, no host step)
+            epoch = self._next_epoch()
+            pv, pb = (pend[0].data_ptr(), pend[1].data_ptr()) if pend else (None, None)
+            native.check(L.mpc_episode_p2p_step(
+                ctypes.byref(self.cfg), self.state.data_ptr(), epoch,
+                self._prev_epoch if pend is not None else 0, v.data_ptr(), b.data_ptr(),
+                self.n_local, self.n_steps, self.lo, self._integ, ws.data_ptr(),
+                ws_prev.data_ptr(), ws.numel(), pv, pb, ctypes.c_void_p(self._mailbox),
+                self.world, self.winner.data_ptr(), self.log.data_ptr(), self.log_capacity, st),
+                "mpc_episode_p2p_step")
+            self._pending = (v, b)
+            self._prev_epoch = epoch
         elif not self.overlap:
             # one launch (selection of step k-1 over the gathered candidates +
             # the rollout of step k + this rank's candidate), then ONE
@@ -409,7 +529,9 @@ class DeviceEpisode:
         self._ws.reverse()
 
     def _next_epoch(self):
-        self._epoch = self._epoch % 0xFFFFFFFF + 1      # nonzero, differs from the last
+        # nonzero, differs from the last and in parity (the P2P mailbox's two
+        # slots alternate: 0xFFFFFFFE is followed by 1)
+        self._epoch = self._epoch % 0xFFFFFFFE + 1
         return self._epoch
 
     def flush(self):
@@ -425,6 +547,14 @@ class DeviceEpisode:
                 self.lo, self._integ, self._ws[1].data_ptr(), self._ws[1].numel(),
                 self.local.data_ptr(), ctypes.byref(self.cfg), self.log.data_ptr(),
                 self.log_capacity, st), "mpc_episode_finalize")
+        elif self.p2p:
+            v, b = pend
+            native.check(L.mpc_episode_p2p_flush(
+                ctypes.byref(self.cfg), self.state.data_ptr(), self._prev_epoch, v.data_ptr(),
+                b.data_ptr(), self.n_local, self.n_steps, self.lo, self._integ,
+                self._ws[1].data_ptr(), self._ws[1].numel(), ctypes.c_void_p(self._mailbox),
+                self.world, self.winner.data_ptr(), self.log.data_ptr(), self.log_capacity, st),
+                "mpc_episode_p2p_flush")
         else:
             if self.overlap:                      # the last collective, then its step
                 torch.cuda.current_stream().wait_stream(self._comm)

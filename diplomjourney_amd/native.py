@@ -41,6 +41,11 @@ EXPORTS = (
     "mpc_episodes_state_bytes", "mpc_episodes_reset", "mpc_episodes_run",
     "mpc_episode_exchange_step2", "mpc_episode_exchange_mark",
     "mpc_stream_create_cu_reserved", "mpc_stream_destroy",
+    "mpc_mailbox_bytes", "mpc_mailbox_alloc", "mpc_mailbox_free", "mpc_mailbox_set_peers",
+    "mpc_mailbox_ping",
+    "mpc_ipc_handle",
+    "mpc_ipc_open", "mpc_ipc_close", "mpc_peer_enable", "mpc_episode_p2p_step",
+    "mpc_episode_p2p_flush",
 )
 
 HIPCC_FLAGS = [
@@ -200,6 +205,33 @@ def lib():
     L.mpc_episode_rollout.restype = ctypes.c_int
     L.mpc_episode_rollout.argtypes = [_P, _P, _P, _I64, _I32, _I64, _I32, _P, ctypes.c_size_t,
                                       _P, ctypes.POINTER(MpcEpisodeConfig), _P, _I32, _P]
+    if not (_LIB_OVERRIDE and not hasattr(L, "mpc_episode_p2p_step")):
+        L.mpc_mailbox_bytes.restype = ctypes.c_size_t
+        L.mpc_mailbox_bytes.argtypes = [_I32]
+        L.mpc_mailbox_alloc.restype = ctypes.c_int
+        L.mpc_mailbox_alloc.argtypes = [_I32, _I32, ctypes.POINTER(_P)]
+        L.mpc_mailbox_free.restype = ctypes.c_int
+        L.mpc_mailbox_free.argtypes = [_P]
+        L.mpc_ipc_handle.restype = ctypes.c_int
+        L.mpc_ipc_handle.argtypes = [_P, _P]
+        L.mpc_ipc_open.restype = ctypes.c_int
+        L.mpc_ipc_open.argtypes = [_P, ctypes.POINTER(_P)]
+        L.mpc_ipc_close.restype = ctypes.c_int
+        L.mpc_ipc_close.argtypes = [_P]
+        L.mpc_peer_enable.restype = ctypes.c_int
+        L.mpc_peer_enable.argtypes = [_I32]
+        L.mpc_mailbox_ping.restype = ctypes.c_int
+        L.mpc_mailbox_ping.argtypes = [_P, ctypes.c_uint32, _P, _P]
+        L.mpc_mailbox_set_peers.restype = ctypes.c_int
+        L.mpc_mailbox_set_peers.argtypes = [_P, _I32, _I32, ctypes.POINTER(_P)]
+        L.mpc_episode_p2p_step.restype = ctypes.c_int
+        L.mpc_episode_p2p_step.argtypes = [
+            ctypes.POINTER(MpcEpisodeConfig), _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _I64,
+            _I32, _I64, _I32, _P, _P, ctypes.c_size_t, _P, _P, _P, _I32, _P, _P, _I32, _P]
+        L.mpc_episode_p2p_flush.restype = ctypes.c_int
+        L.mpc_episode_p2p_flush.argtypes = [
+            ctypes.POINTER(MpcEpisodeConfig), _P, ctypes.c_uint32, _P, _P, _I64, _I32, _I64,
+            _I32, _P, ctypes.c_size_t, _P, _I32, _P, _P, _I32, _P]
     if not (_LIB_OVERRIDE and not hasattr(L, "mpc_episodes_run")):   # (older A/B builds)
         L.mpc_episodes_state_bytes.restype = ctypes.c_size_t
         L.mpc_episodes_state_bytes.argtypes = [_I32]

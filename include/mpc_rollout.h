@@ -376,6 +376,60 @@ int mpc_episode_exchange_flush(const mpc_episode_config_t* cfg, void* state, int
                                const mpc_candidate_t* gathered, int32_t n_gathered,
                                mpc_result_t* out, mpc_episode_log_t* log, int32_t log_capacity,
                                mpc_stream_t stream);
+/* Multi-GPU chained step WITHOUT a collective (SURVEY §8e over xGMI): the
+ * per-rank candidates travel by peer stores from the launches themselves, and
+ * the exchange of step k runs inside launch k+1 beside its rollout.  Every
+ * rank owns a mailbox (mpc_mailbox_alloc: mpc_mailbox_bytes(world) bytes of
+ * its HBM, zeroed; uncached = 1 makes every access go to HBM, which is what
+ * peer stores over xGMI need to be seen) whose header holds the world
+ * mailboxes as mapped in this process (mpc_mailbox_set_peers, once, before
+ * the first step; peers[rank] = this mailbox): another process's via
+ * mpc_ipc_handle (on its rank) + mpc_ipc_open (here), another GPU of this
+ * process directly after mpc_peer_enable.  Per MPC step each rank launches
+ *   mpc_episode_p2p_step(epoch, prev_epoch = the previous step's epoch, 0 on
+ *   the first step of a chain) — the structure of mpc_episode_chain_step
+ *   (ws / ws_prev alternated, the previous step's controls v_prev / beta_prev)
+ *   whose block 0 reduces the previous launch's block records into this
+ *   rank's candidate, stores it into slot prev_epoch & 1 of every rank's
+ *   mailbox (then the tags), waits (bounded, ~1 s; chain error 5) for the
+ *   world candidates in its own mailbox, selects the (cost, global index)
+ *   minimum, re-rolls it into out_prev (the global winner, on every rank),
+ *   updates the episode and publishes this step's constants; the tile blocks
+ *   meanwhile roll out this rank's shard (index_base).
+ * Consecutive epochs must differ in parity (the two slots alternate); every
+ * rank runs the same sequence of epochs.  The chain ends with
+ * mpc_episode_p2p_flush (the last step's controls and workspace).  No host
+ * step and no collective between launches: plain kernels on one stream,
+ * graph-capturable (end a captured sequence with the flush, as above).
+ * world <= 32. */
+#define MPC_IPC_HANDLE_BYTES 64
+size_t mpc_mailbox_bytes(int32_t world);
+int mpc_mailbox_alloc(int32_t world, int32_t uncached, void** mailbox);
+int mpc_mailbox_free(void* mailbox);
+int mpc_mailbox_set_peers(void* mailbox, int32_t rank, int32_t world, const void* const* peers);
+/* Self-test of the mailboxes (every rank, after every rank's set_peers, e.g.
+ * behind a barrier): each rank stores `tag` into every rank's ping word and
+ * waits (~0.1 s at most) for all of its own; *ok (device int32) = 1 if all
+ * arrived.  A host that gets 0 on any rank uses the all_gather exchange. */
+int mpc_mailbox_ping(void* mailbox, uint32_t tag, int32_t* ok, mpc_stream_t stream);
+int mpc_ipc_handle(void* dev_ptr, void* handle /* MPC_IPC_HANDLE_BYTES */);
+int mpc_ipc_open(const void* handle, void** dev_ptr);
+int mpc_ipc_close(void* dev_ptr);
+int mpc_peer_enable(int32_t peer_device);
+int mpc_episode_p2p_step(const mpc_episode_config_t* cfg, void* state, uint32_t epoch,
+                         uint32_t prev_epoch, const double* v_sc, const double* beta_sc,
+                         int64_t n_cand, int32_t n_steps, int64_t index_base, int32_t integrator,
+                         void* ws, const void* ws_prev, size_t ws_bytes, const double* v_prev,
+                         const double* beta_prev, void* mailbox, int32_t world,
+                         mpc_result_t* out_prev, mpc_episode_log_t* log, int32_t log_capacity,
+                         mpc_stream_t stream);
+int mpc_episode_p2p_flush(const mpc_episode_config_t* cfg, void* state, uint32_t last_epoch,
+                          const double* v_last, const double* beta_last, int64_t n_cand,
+                          int32_t n_steps, int64_t index_base, int32_t integrator,
+                          const void* ws_last, size_t ws_bytes, void* mailbox, int32_t world,
+                          mpc_result_t* out, mpc_episode_log_t* log, int32_t log_capacity,
+                          mpc_stream_t stream);
+
 /* The exchange's collective for a non-Python host: an RCCL
  * communicator per GPU — one process driving all local GPUs (a clique,
  * mpc_comm_init_all) or one rank per process (mpc_comm_unique_id on rank 0,

@@ -146,3 +146,58 @@ def test_no_cpu_fallback(monkeypatch, tmp_path):
     monkeypatch.setattr(native, "_LIB_OVERRIDE", str(tmp_path / "missing.so"))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         native.lib()
+
+
+def test_p2p_exchange_argument_validation_without_gpu():
+    """mpc_mailbox_* / mpc_ipc_* / mpc_episode_p2p_*: sizes and rejected
+    arguments, before any HIP call."""
+    from diplomjourney_amd.episode import reference_episode_config
+    L = native.lib()
+    assert L.mpc_mailbox_bytes(0) == 0 and L.mpc_mailbox_bytes(33) == 0
+    one, eight = L.mpc_mailbox_bytes(1), L.mpc_mailbox_bytes(8)
+    # header (32 peer pointers, rank, world, 32 ping words; 256-B padded), tag
+    # words, then two slots of one 64-B-padded candidate per rank
+    rec = (abi.CANDIDATE_BYTES + 63) // 64 * 64
+    hdr = one - 2 * 32 * 8 - 2 * rec
+    assert eight - one == 2 * 7 * rec and hdr % 256 == 0 and hdr >= 32 * 8 * 2 + 8
+    out = ctypes.c_void_p()
+    assert L.mpc_mailbox_alloc(0, 1, ctypes.byref(out)) == abi.MPC_ERR_ARG
+    assert L.mpc_mailbox_alloc(2, 1, None) == abi.MPC_ERR_ARG
+    assert L.mpc_mailbox_free(None) == abi.MPC_ERR_ARG
+    assert L.mpc_ipc_handle(None, None) == abi.MPC_ERR_ARG
+    assert L.mpc_ipc_open(None, ctypes.byref(out)) == abi.MPC_ERR_ARG
+    assert L.mpc_ipc_close(None) == abi.MPC_ERR_ARG
+    f = ctypes.c_void_p(0x1000)
+    g = ctypes.c_void_p(0x2000)
+    peers = (ctypes.c_void_p * 2)(f, g)
+    assert L.mpc_mailbox_set_peers(None, 0, 2, peers) == abi.MPC_ERR_ARG
+    assert L.mpc_mailbox_set_peers(f, 2, 2, peers) == abi.MPC_ERR_ARG
+    assert L.mpc_mailbox_set_peers(f, 1, 2, peers) == abi.MPC_ERR_ARG   # own row != mailbox
+    assert L.mpc_mailbox_set_peers(f, 0, 33, peers) == abi.MPC_ERR_ARG
+    assert L.mpc_mailbox_ping(None, 1, f, None) == abi.MPC_ERR_ARG
+    assert L.mpc_mailbox_ping(f, 0, f, None) == abi.MPC_ERR_ARG
+    assert L.mpc_mailbox_ping(f, 1, None, None) == abi.MPC_ERR_ARG
+    cfg = reference_episode_config()
+    ig = abi.INTEGRATORS["rect+cum"]
+
+    def step(epoch=3, prev=2, mailbox=f, world=2, out_prev=f, ws_prev=f, v_prev=f):
+        return L.mpc_episode_p2p_step(ctypes.byref(cfg), f, epoch, prev, f, f, 1024, 10, 0, ig,
+                                      f, ws_prev, 1 << 20, v_prev, f, mailbox, world, out_prev,
+                                      f, 8, None)
+    assert step(epoch=0) == abi.MPC_ERR_ARG
+    assert step(prev=1) == abi.MPC_ERR_ARG             # same parity: same mailbox slot
+    assert step(mailbox=None) == abi.MPC_ERR_ARG
+    assert step(world=0) == abi.MPC_ERR_ARG
+    assert step(world=33) == abi.MPC_ERR_ARG
+    assert step(out_prev=None) == abi.MPC_ERR_ARG      # a previous step to complete ...
+    assert step(ws_prev=None) == abi.MPC_ERR_ARG       # ... from its records
+    assert step(v_prev=None) == abi.MPC_ERR_ARG        # ... and controls
+
+    def flush(epoch=3, mailbox=f, world=2, out=f, ws=f):
+        return L.mpc_episode_p2p_flush(ctypes.byref(cfg), f, epoch, f, f, 1024, 10, 0, ig, ws,
+                                       1 << 20, mailbox, world, out, f, 8, None)
+    assert flush(epoch=0) == abi.MPC_ERR_ARG
+    assert flush(mailbox=None) == abi.MPC_ERR_ARG
+    assert flush(world=0) == abi.MPC_ERR_ARG
+    assert flush(out=None) == abi.MPC_ERR_ARG
+    assert flush(ws=None) == abi.MPC_ERR_ARG

@@ -393,6 +393,10 @@ def test_exchange_chain_two_ranks_on_one_gpu(engine, tmp_path):
     (two child processes): both ranks log exactly the steps of one rank
     running the single-GPU chained episode over all the candidates, restarts
     and the final global winner included."""
+    _run_two_ranks(engine, tmp_path, "gather")
+
+
+def _run_two_ranks(engine, tmp_path, mode):
     import json
     import os
     import socket
@@ -407,7 +411,7 @@ def test_exchange_chain_two_ranks_on_one_gpu(engine, tmp_path):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     procs = [subprocess.Popen([sys.executable, os.path.join(repo, "tests", "dist_rank.py"),
                                str(r), str(world), str(port), str(n_total), str(ns), str(steps),
-                               str(tmp_path / f"rank{r}.json")], env=env,
+                               str(tmp_path / f"rank{r}.json"), mode], env=env,
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
              for r in range(world)]
     outs = [p.communicate(timeout=240)[0] for p in procs]
@@ -994,6 +998,59 @@ def test_chained_exchange_path_and_graph_capture(engine, wheelbase, n, cap, over
             dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("wheelbase,n,cap", [(0.5, 40_000, 6), (0.45, 40_000, 6),
+                                             (0.5, 1_000_000, 3)])
+def test_p2p_exchange_one_rank_eager_and_graph(engine, wheelbase, n, cap):
+    """The collective-free exchange (mpc_episode_p2p_step: block 0 posts the
+    rank's candidate into every rank's mailbox and the next launch's block 0
+    waits for them in its own) on one rank: eager steps, then a captured
+    sequence (ending with mpc_episode_p2p_flush) replayed three times, log the
+    steps of the single-GPU episode.  A replay repeats its launches' epochs,
+    so it passes only if every consumed mailbox tag was cleared."""
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.episode import DeviceEpisode
+    ns, steps, reps = 10, 12, 3
+    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
+    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
+    pool = [engine.sample_controls(V, B, n, ns, 1900 + i) for i in range(steps)]
+    half = steps - cap
+    ref = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64, L=wheelbase)
+    for i in list(range(steps)) + list(range(half, steps)) * (reps - 1):
+        ref.step(controls=pool[i])
+    want = _episode_log(ref)
+    ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64, exchange=True,
+                       chain=True, L=wheelbase, p2p=True)
+    try:
+        for i in range(half):
+            ep.step(controls=pool[i])
+        ep.flush()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        n0 = ep.steps_enqueued
+        with torch.cuda.graph(g):
+            for i in range(half, steps):
+                ep.step(controls=pool[i])
+            ep.flush()
+        ep.steps_enqueued = n0
+        for _ in range(reps):
+            g.replay()
+            ep.steps_enqueued += steps - half
+        torch.cuda.synchronize()
+        assert _episode_log(ep) == want
+        assert ep.chain_error() == 0
+    finally:
+        ep.close()
+
+
+def test_p2p_exchange_two_ranks_on_one_gpu(engine, tmp_path):
+    """The collective-free exchange with 2 ranks (two processes sharing this
+    GPU; the mailboxes' IPC handles exchanged once over gloo, every step's
+    candidates by the launches' own peer stores): both ranks log exactly the
+    steps of one rank running the single-GPU chained episode over all the
+    candidates, restarts and the final global winner included."""
+    _run_two_ranks(engine, tmp_path, "p2p")
+
+
 def test_overlapped_exchange_with_a_late_collective(engine):
     """The overlapped exchange step (mpc_episode_exchange_step2): the
     all_gather of step k runs on a side stream beside launch k+1, whose block
@@ -1088,7 +1145,8 @@ def test_bench_contract(extra):
     assert rf["traffic"] is not None and abs(rf["traffic"] / 160e6 - 1) < 0.01
 
 
-def test_bench_two_ranks_spawned():
+@pytest.mark.parametrize("mode", ["p2p", "rccl"])
+def test_bench_two_ranks_spawned(mode):
     """`python bench.py --gpus 2` with no launcher (the driver's own command
     form) runs TWO ranks — spawned by the GPU-free parent, here rehearsed
     with gloo on the one GPU — and rank 0's line says so: n_gpus 2, the
@@ -1101,7 +1159,8 @@ def test_bench_two_ranks_spawned():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2",
                         "--dist-backend", "gloo", "--candidates-per-gpu", "100000", "--steps", "8",
-                        "--warmup", "2", "--cpu-seconds", "0", "--no-second-pass"],
+                        "--warmup", "2", "--cpu-seconds", "0", "--no-second-pass",
+                        "--exchange-mode", mode],
                        capture_output=True, text=True, timeout=110, cwd=repo, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -1109,9 +1168,14 @@ def test_bench_two_ranks_spawned():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["chain_error"] == 0 and d["value"] > 0
     assert d["config"]["candidates_total"] == 200_000 and d["scaling"] == "weak"
-    assert "all_gather(536 B candidates)" in d["config"]["parallelism"]
+    if mode == "p2p":   # the mailboxes' self-test passed: no fallback
+        assert "peer stores" in d["config"]["parallelism"]
+        assert d["exchange"] == "mailbox peer stores"
+    else:
+        assert "all_gather(536 B candidates)" in d["config"]["parallelism"]
     rf = d["roofline"]
-    assert rf["kernel"] == "k_episode_chain[exchange]" and 0 < rf["frac"] < 1
+    assert rf["kernel"] == ("k_episode_chain[p2p]" if mode == "p2p"
+                            else "k_episode_chain[exchange]") and 0 < rf["frac"] < 1
     assert rf["algorithmic_bytes_per_launch"] == 16.0 * 10 * 100_000
 
 
