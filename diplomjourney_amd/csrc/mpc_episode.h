@@ -880,21 +880,28 @@ __device__ __forceinline__ bool chain_read(const EpisodeState* S, uint32_t epoch
 // each access goes to HBM, so stores a peer GPU makes over xGMI are what this
 // GPU's loads see).  Block 0 of rank q's launch with epoch e+1 — the launch
 // that completes step e — reduces step e's block records (the previous
-// launch's, stream-ordered: plain loads), stores q's candidate into slot e&1,
-// row q, of EVERY rank's mailbox (its own included) and then, behind its
-// stores' completion, the tag e into that mailbox's tag word (slot, q); it
-// then waits for the `world` tags of slot e&1 in its own mailbox, stages the
-// candidates in LDS, clears the tags, selects the global winner and updates
-// the episode.  The tile blocks meanwhile stream step e+1 (its constants are
+// launch's, stream-ordered: plain loads) into q's candidate and stores it into
+// slot e&1, row q, of EVERY rank's mailbox (its own included); it then waits
+// until the world's candidates of step e are complete in its own mailbox,
+// stages them in LDS, clears them, selects the global winner and updates the
+// episode.  The tile blocks meanwhile stream step e+1 (its constants are
 // speculated until block 0 publishes them, as in the one-GPU chain): the
 // exchange runs beside the rollout, not between launches.
-// Two slots suffice: rank q writes slot e&1 again only for step e+2, after it
-// has read every rank's step-(e+1) candidate — each of which its writer
-// posted after clearing its own slot-(e&1) tags.  Accesses are 8-B relaxed
-// system-scope atomics (`sc0 sc1`).
+// Self-validating granules: each 8-B word of a candidate travels as one 16-B
+// granule whose two 8-B halves both carry the step's 16-bit tag (word[63:16]
+// | tag, word[15:0] << 48 | tag — the tagged block records' encoding), so a
+// reader accepts a word only when both halves are this step's, never relying
+// on store ordering, on a fence or on 16-B single-copy atomicity: the writer
+// issues its stores and goes on (no completion wait, no flag store), the
+// reader polls the granules themselves.  Only the words a step needs move:
+// cost, index, (n_steps, reserved), v[0..n_steps), beta[0..n_steps).
+// A consumed granule is zeroed by its reader.  Two slots suffice: rank q
+// writes slot e&1 again only for step e+2, after it has read every rank's
+// step-(e+1) candidate — each posted in a launch that began after the launch
+// whose zeroing stores had completed (a kernel boundary).
 //   layout: MailHdr (the peers' mailbox pointers as mapped in this process,
-//           this rank, the world size), uint64 tag[2][kMailMaxRanks], then
-//           record[2][world] of kMailRecBytes (an mpc_candidate_t, padded)
+//           this rank, the world size, ping words), then granule
+//           [2][world][kCandWords] of 16 B
 constexpr int kMailMaxRanks = kXchgLdsRanks;
 struct MailHdr {
   uint64_t peers[kMailMaxRanks];
@@ -902,26 +909,28 @@ struct MailHdr {
   uint64_t ping[kMailMaxRanks];   // mpc_mailbox_ping: rank r's ping word
 };
 constexpr size_t kMailHdrBytes = (sizeof(MailHdr) + 255) & ~size_t{255};
-constexpr size_t kMailTagBytes = 2 * kMailMaxRanks * sizeof(uint64_t);
-constexpr size_t kMailRecBytes = (sizeof(mpc_candidate_t) + 63) & ~size_t{63};
 constexpr int kCandWords = static_cast<int>(sizeof(mpc_candidate_t) / 8);
+constexpr size_t kMailRecBytes = kCandWords * sizeof(u64x2);
 static_assert(sizeof(mpc_candidate_t) % 8 == 0, "candidates move as 8-B words");
+static_assert(offsetof(mpc_candidate_t, v) == 24 && offsetof(mpc_candidate_t, beta) ==
+                  24 + 8 * MPC_MAX_STEPS, "candidate word map (cand_word)");
 // Peers' launches are not stream-ordered with this one: a rank may start its
 // step a host-side hiccup later.  ~1 s before chain error 5.
 constexpr uint32_t kP2PSpinLimit = 1u << 24;
 
 __host__ __device__ inline size_t mailbox_bytes(int world) {
-  return kMailHdrBytes + kMailTagBytes + 2 * static_cast<size_t>(world) * kMailRecBytes;
+  return kMailHdrBytes + 2 * static_cast<size_t>(world) * kMailRecBytes;
 }
 
-__device__ __forceinline__ uint64_t* mail_tag(void* mb, uint32_t slot, int rank) {
-  return reinterpret_cast<uint64_t*>(static_cast<char*>(mb) + kMailHdrBytes) +
-         slot * kMailMaxRanks + rank;
+__device__ __forceinline__ u64x2* mail_rec(void* mb, uint32_t slot, int rank, int world) {
+  return reinterpret_cast<u64x2*>(static_cast<char*>(mb) + kMailHdrBytes +
+                                  (static_cast<size_t>(slot) * world + rank) * kMailRecBytes);
 }
 
-__device__ __forceinline__ uint64_t* mail_rec(void* mb, uint32_t slot, int rank, int world) {
-  return reinterpret_cast<uint64_t*>(static_cast<char*>(mb) + kMailHdrBytes + kMailTagBytes +
-                                     (static_cast<size_t>(slot) * world + rank) * kMailRecBytes);
+// The j-th posted word of a candidate of n_steps steps: its word index in
+// mpc_candidate_t (3 header words, then v[0..n), then beta[0..n)).
+__device__ __forceinline__ int cand_word(int j, int n_steps) {
+  return j < 3 + n_steps ? j : j + (MPC_MAX_STEPS - n_steps);
 }
 
 // Where block 0 stages candidates: the control ring's LDS after the re-roll's
@@ -934,7 +943,9 @@ __device__ __forceinline__ mpc_candidate_t* cand_lds() {
 // Block 0, all threads: this rank's best candidate of the previous launch —
 // the lexicographic (cost, local index) minimum of its n_part block records
 // (plain 16-B records of a stream-ordered earlier launch), its global index
-// and its controls — into `out` (LDS).
+// and its controls — into `out` (LDS).  Each wave loads its own best's
+// controls while the waves' minima are combined (finalize_block's prefetch:
+// no dependent load after the block's winner is known).
 __device__ void records_candidate(const Rec* __restrict__ part, int n_part,
                                   const double* __restrict__ v, const double* __restrict__ b,
                                   int64_t n_cand, int n_steps, int64_t index_base,
@@ -954,23 +965,36 @@ __device__ void records_candidate(const Rec* __restrict__ part, int n_part,
       k = r[q].key;
       i = r[q].idx;
     }
-  block_argmin(k, i);
-  __shared__ uint64_t s_k;
-  __shared__ int64_t s_i;
-  if (threadIdx.x == 0) {
-    s_k = k;
-    s_i = i;
+  wave_argmin(k, i);   // every lane: its wave's best
+  const int ln = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double pv = 0.0, pb = 0.0;
+  if (k != ~0ull && ln < n_steps) {
+    pv = v[ln * n_cand + i];
+    pb = b[ln * n_cand + i];
+  }
+  __shared__ uint64_t s_k[kWaves];
+  __shared__ int64_t s_i[kWaves];
+  if (ln == 0) {
+    s_k[wave] = k;
+    s_i[wave] = i;
   }
   __syncthreads();
-  k = s_k;
-  i = s_i;
+  int wbest = 0;
+  k = s_k[0];
+  i = s_i[0];
+#pragma unroll
+  for (int w = 1; w < kWaves; ++w)
+    if (rec_less(s_k[w], s_i[w], k, i)) {
+      k = s_k[w];
+      i = s_i[w];
+      wbest = w;
+    }
   const bool valid = k != ~0ull;
-  const int q = threadIdx.x;
-  if (q < MPC_MAX_STEPS) {   // one value per lane
-    out->v[q] = (valid && q < n_steps) ? v[q * n_cand + i] : 0.0;
-    out->beta[q] = (valid && q < n_steps) ? b[q * n_cand + i] : 0.0;
+  if (wave == wbest && ln < MPC_MAX_STEPS) {   // one value per lane
+    out->v[ln] = (valid && ln < n_steps) ? pv : 0.0;
+    out->beta[ln] = (valid && ln < n_steps) ? pb : 0.0;
   }
-  if (q == 0) {
+  if (threadIdx.x == 0) {
     out->cost = valid ? key_cost(k) : __builtin_inf();
     out->index = valid ? index_base + i : -1;
     out->n_steps = n_steps;
@@ -978,66 +1002,70 @@ __device__ void records_candidate(const Rec* __restrict__ part, int n_part,
   }
 }
 
-// Block 0, all threads: post this rank's candidate (in LDS) of step `tag` to
-// every rank's mailbox: the record words, every storing wave's wait for its
-// stores, a barrier, then one tag store per rank.
-__device__ void post_candidate(void* mb, int world, uint32_t tag, const mpc_candidate_t* cand) {
-  const uint32_t slot = tag & 1u;
-  const MailHdr* hdr = static_cast<const MailHdr*>(mb);
-  const int rank = hdr->rank;
+// Block 0, all threads: post this rank's candidate (in LDS) of step `epoch`
+// to every rank's mailbox as tagged granules (16-B `sc0 sc1` stores; nothing
+// waits for them).
+__device__ void post_candidate(const uint64_t* s_peers, int rank, int world, uint32_t epoch,
+                               int n_steps, const mpc_candidate_t* cand) {
+  const uint32_t slot = epoch & 1u;
+  const uint64_t tag = rec_tag(epoch);
+  const int words = 3 + 2 * n_steps;
   __syncthreads();   // the candidate is complete in LDS
   const uint64_t* src = reinterpret_cast<const uint64_t*>(cand);
-  for (int q = threadIdx.x; q < world * kCandWords; q += blockDim.x) {
-    const int r = q / kCandWords, w = q - r * kCandWords;
-    void* peer = reinterpret_cast<void*>(hdr->peers[r]);
-    __hip_atomic_store(mail_rec(peer, slot, rank, world) + w, src[w], __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+  for (int q = threadIdx.x; q < world * words; q += blockDim.x) {
+    const int r = q / words, j = q - r * words;
+    const uint64_t w = src[cand_word(j, n_steps)];
+    u64x2* dst = mail_rec(reinterpret_cast<void*>(s_peers[r]), slot, rank, world) + j;
+    // (s_nop 1: the store reads its data registers before hipcc's next
+    // instruction may overwrite them)
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1"
+                 :
+                 : "v"(dst), "v"(u64x2{(w & ~0xffffull) | tag, (w << 48) | tag})
+                 : "memory");
   }
-  // (the tag-clearing stores of the previous wait_mailbox are among the
-  // waited ones: a peer sees this step's candidate only after they completed)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (static_cast<int>(threadIdx.x) < world)
-    __hip_atomic_store(mail_tag(reinterpret_cast<void*>(hdr->peers[threadIdx.x]), slot, rank),
-                       static_cast<uint64_t>(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Block 0, all threads: wait (bounded; chain error 5) for every rank's
-// candidate of step `tag` in this rank's mailbox, copy them into LDS
-// (cand_lds) and clear the tags.  Returns the LDS copy, or nullptr on a
-// timeout.
-__device__ const mpc_candidate_t* wait_mailbox(EpisodeState* S, void* mb, uint32_t tag,
-                                               int world) {
-  __shared__ int s_ok;
-  const uint32_t slot = tag & 1u;
-  if (threadIdx.x < 64) {   // wave 0; lane r watches rank r's tag
-    bool seen = static_cast<int>(threadIdx.x) >= world;
-    uint32_t it = 0;
-    for (; it < kP2PSpinLimit; ++it) {
-      if (!seen)
-        seen = static_cast<uint32_t>(__hip_atomic_load(mail_tag(mb, slot, threadIdx.x),
-                                                       __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_SYSTEM)) == tag;
-      if (__ballot(!seen) == 0) break;   // (uniform over the wave)
+// Block 0, all threads: wait (bounded; chain error 5) until every rank's
+// candidate of step `epoch` is complete in this rank's mailbox, decode them
+// into LDS (cand_lds) and zero the granules.  Returns the LDS copy, or nullptr
+// on a timeout.
+__device__ const mpc_candidate_t* wait_mailbox(EpisodeState* S, void* mb, uint32_t epoch,
+                                               int world, int n_steps) {
+  const uint32_t slot = epoch & 1u;
+  const uint32_t tag = rec_tag(epoch);
+  const int words = 3 + 2 * n_steps, total = world * words;
+  mpc_candidate_t* dst = cand_lds();
+  uint32_t it = 0;
+  // one granule per thread and pass (world * words <= 256 in one pass: up to
+  // 11 ranks at N = 10); a later chunk is polled after the earlier is in
+#pragma unroll 1
+  for (int base = 0; base < total; base += kBlock) {
+    const int q = base + static_cast<int>(threadIdx.x);
+    const int r = q / words, j = q - r * words;
+    uint64_t* h = q < total ? reinterpret_cast<uint64_t*>(mail_rec(mb, slot, r, world) + j)
+                            : nullptr;
+    u64x2 g = {0, 0};
+    for (;; ++it) {
+      bool ok = true;
+      if (h) {
+        g.x = __hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        g.y = __hip_atomic_load(h + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok = tagged_rec_fresh(g, tag);
+      }
+      if (__syncthreads_and(ok)) break;   // uniform: every thread counts the same passes
+      if (it >= kP2PSpinLimit) {
+        if (threadIdx.x == 0) S->chain_error = 5u;
+        return nullptr;
+      }
       __builtin_amdgcn_s_sleep(1);
     }
-    if (threadIdx.x == 0) {
-      s_ok = it < kP2PSpinLimit;
-      if (it >= kP2PSpinLimit) S->chain_error = 5u;
+    if (h) {
+      reinterpret_cast<uint64_t*>(&dst[r])[cand_word(j, n_steps)] = tagged_rec_key(g);
+      __hip_atomic_store(h, uint64_t{0}, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(h + 1, uint64_t{0}, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   __syncthreads();
-  if (!s_ok) return nullptr;
-  mpc_candidate_t* dst = cand_lds();
-  for (int q = threadIdx.x; q < world * kCandWords; q += blockDim.x) {
-    const int r = q / kCandWords, w = q - r * kCandWords;
-    reinterpret_cast<uint64_t*>(dst)[q] = __hip_atomic_load(
-        mail_rec(mb, slot, r, world) + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  __syncthreads();   // every load has returned (its value is in LDS)
-  if (static_cast<int>(threadIdx.x) < world)
-    __hip_atomic_store(mail_tag(mb, slot, threadIdx.x), uint64_t{0}, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
   return dst;
 }
 
@@ -1052,10 +1080,20 @@ __device__ void p2p_complete(const mpc_episode_config_t& c, EpisodeState* S, voi
                              int64_t n_cand, int n_steps, int64_t index_base,
                              mpc_result_t* __restrict__ out_prev,
                              mpc_episode_log_t* __restrict__ log, int cap, uint32_t publish_epoch) {
+  // the header (peers, rank: uncached, so a full memory round trip) loaded
+  // before the records, its values parked in LDS after them
+  __shared__ uint64_t s_peers[kMailMaxRanks];
+  __shared__ int s_rank;
+  const MailHdr* hdr = static_cast<const MailHdr*>(mb);
+  const uint64_t my_peer = static_cast<int>(threadIdx.x) < world ? hdr->peers[threadIdx.x] : 0;
+  const int my_rank = threadIdx.x == 0 ? hdr->rank : 0;
   mpc_candidate_t* lc = cand_lds();
   records_candidate(part_prev, n_part_prev, v_prev, b_prev, n_cand, n_steps, index_base, lc);
-  post_candidate(mb, world, prev, lc);
-  const mpc_candidate_t* g = wait_mailbox(S, mb, prev, world);
+  if (static_cast<int>(threadIdx.x) < world) s_peers[threadIdx.x] = my_peer;
+  if (threadIdx.x == 0) s_rank = my_rank;
+  __syncthreads();
+  post_candidate(s_peers, s_rank, world, prev, n_steps, lc);
+  const mpc_candidate_t* g = wait_mailbox(S, mb, prev, world, n_steps);
   if (g) {
     advance_from_candidates<INTEG, ROT>(c, S, g, world, out_prev, log, cap, publish_epoch,
                                         ring_lds());

@@ -155,10 +155,10 @@ def test_p2p_exchange_argument_validation_without_gpu():
     L = native.lib()
     assert L.mpc_mailbox_bytes(0) == 0 and L.mpc_mailbox_bytes(33) == 0
     one, eight = L.mpc_mailbox_bytes(1), L.mpc_mailbox_bytes(8)
-    # header (32 peer pointers, rank, world, 32 ping words; 256-B padded), tag
-    # words, then two slots of one 64-B-padded candidate per rank
-    rec = (abi.CANDIDATE_BYTES + 63) // 64 * 64
-    hdr = one - 2 * 32 * 8 - 2 * rec
+    # header (32 peer pointers, rank, world, 32 ping words; 256-B padded), then
+    # two slots of one candidate per rank, each 8-B word as a 16-B tagged granule
+    rec = abi.CANDIDATE_BYTES * 2
+    hdr = one - 2 * rec
     assert eight - one == 2 * 7 * rec and hdr % 256 == 0 and hdr >= 32 * 8 * 2 + 8
     out = ctypes.c_void_p()
     assert L.mpc_mailbox_alloc(0, 1, ctypes.byref(out)) == abi.MPC_ERR_ARG

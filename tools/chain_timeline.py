@@ -4,7 +4,8 @@ sources (the shipped sources carry none), then one chained step among
 back-to-back ones, decoded per phase.
 
     python tools/chain_timeline.py build            # -> tools/var_timeline.so (CPU)
-    python tools/chain_timeline.py run N_CAND N     # on the GPU box
+    python tools/chain_timeline.py run N_CAND N [p2p]   # on the GPU box (p2p: the
+                                                    # one-rank P2P exchange form)
 
 Block 0 (completion of step k-1): entry, records loaded + lane minima, wave
 arg-min, block winner (after the barrier), winner re-rolled (emit_winner),
@@ -73,6 +74,17 @@ def build():
     ])
     t = lambda q: f"if (threadIdx.x == 0) {STAMP.format(slot=f'8 * blockIdx.x + {q}')};"   # noqa: E731
     patch(os.path.join(cs, "mpc_episode.h"), [
+        # P2P block 0 (p2p_complete): candidate from the records, posted, the
+        # world's gathered; published (advance_from_candidates' store_update)
+        ("  records_candidate(part_prev, n_part_prev, v_prev, b_prev, n_cand, n_steps, index_base, lc);\n",
+         "  records_candidate(part_prev, n_part_prev, v_prev, b_prev, n_cand, n_steps, index_base, lc);\n"
+         f"  {b0(1)}\n"),
+        ("  post_candidate(s_peers, s_rank, world, prev, n_steps, lc);\n",
+         f"  post_candidate(s_peers, s_rank, world, prev, n_steps, lc);\n  {b0(2)}\n"),
+        ("  const mpc_candidate_t* g = wait_mailbox(S, mb, prev, world, n_steps);\n",
+         f"  const mpc_candidate_t* g = wait_mailbox(S, mb, prev, world, n_steps);\n  {b0(3)}\n"),
+        ("               kPubWords, publish_epoch);\n  emit_winner_tail",
+         f"               kPubWords, publish_epoch);\n  {b0(8)}\n  emit_winner_tail"),
         ("  L.status = status;\n  if (ended) {\n",
          f"  L.status = status;\n  {b0(6)}\n  if (ended) {{\n"),
         ("  if (blockIdx.x == 0) {\n    if (has_prev) {\n",
@@ -103,7 +115,10 @@ def build():
     print(VAR)
 
 
-def run(n, ns):
+B0_P2P = {1: "candidate", 2: "posted", 3: "gathered", 6: "advance", 8: "published"}
+
+
+def run(n, ns, mode="chain"):
     os.environ["DIPLOMJOURNEY_MPC_LIB"] = VAR
     sys.path.insert(0, REPO)
     import torch
@@ -115,7 +130,9 @@ def run(n, ns):
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
     pool = [eng.sample_controls(V, B, n, ns, 0x5EED0000 + i) for i in range(8)]
-    ep = DeviceEpisode(eng, n, ns, integrator="rect+cum", chain=True, log_capacity=8192)
+    p2p = mode == "p2p"
+    ep = DeviceEpisode(eng, n, ns, integrator="rect+cum", chain=True, log_capacity=8192,
+                       exchange=p2p, p2p=p2p)
     L = native.lib()
     L.mpc_debug_timeline.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     nb = (n + 511) // 512 + 1
@@ -130,7 +147,8 @@ def run(n, ns):
         t0 = min(t[8 * b] for b in range(nb))
         us = lambda x: (x - t0) * 0.01   # noqa: E731
         b0 = {"entry": us(t[0])}
-        b0.update({name: us(buf[B0_BASE + q]) for q, name in enumerate(B0) if q})
+        names = B0_P2P if p2p else {q: name for q, name in enumerate(B0) if q}
+        b0.update({name: us(buf[B0_BASE + q]) for q, name in names.items()})
         row = {"block0": b0}
         for q, name in enumerate(TILE):
             xs = sorted(us(t[8 * b + q]) for b in range(1, nb))
@@ -151,4 +169,4 @@ if __name__ == "__main__":
     if sys.argv[1] == "build":
         build()
     else:
-        run(int(sys.argv[2]), int(sys.argv[3]))
+        run(int(sys.argv[2]), int(sys.argv[3]), *(sys.argv[4:5]))
