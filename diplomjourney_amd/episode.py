@@ -372,7 +372,8 @@ class DeviceEpisode:
                         p = ctypes.c_void_p()
                         hr = (ctypes.c_uint8 * IPC_HANDLE_BYTES).from_buffer_copy(
                             handles[r].tobytes())
-                        native.check(L.mpc_ipc_open(hr, ctypes.byref(p)), "mpc_ipc_open")
+                        with torch.cuda.device(dev):   # mapped for this rank's GPU
+                            native.check(L.mpc_ipc_open(hr, ctypes.byref(p)), "mpc_ipc_open")
                         self._opened.append(p.value)
                         ptrs[r] = p.value
                 arr = (ctypes.c_void_p * self.world)(*ptrs)
