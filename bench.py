@@ -874,16 +874,17 @@ XCHG_KERNEL = "k_episode_chain[exchange]"
 P2P_KERNEL = "k_episode_chain[p2p]"
 TRAFFIC_JSON = {"k_rollout_argmin_stream": "r03_traffic_stream.json",
                 "k_episode_chain": "r03_close/traffic_chain.json",
-                XCHG_KERNEL: "r04/traffic_chain_xchg.json"}
+                XCHG_KERNEL: "r04/traffic_chain_xchg.json",
+                P2P_KERNEL: "r04_close/traffic_chain_p2p.json"}
 
 # fp64 VALU counters (tools/pmc_valu.sh: SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F64,
 # SQ_INSTS_VALU) of each kernel at the size it was measured on:
 # (kernel, integrator) -> (summary, candidates, horizon) — config C, or the
 # S1 = 451 full tree of config F (candidates = leaves)
-VALU_JSON = {("k_episode_chain", "rect+cum"): ("r03_close/valu/chain.json", 1_000_000, 10),
-             ("k_rollout_argmin_stream", "qk21"): ("r03_close/valu/qk21.json", 1_000_000, 10),
-             ("k_rollout_generated", "rect+cum"): ("r03_close/valu/gen.json", 1_000_000, 10),
-             ("k_ft_leaves", "rect+rot"): ("r03_close/valu/ft.json", 451 ** 3, 3)}
+VALU_JSON = {("k_episode_chain", "rect+cum"): ("r04_close/valu/chain.json", 1_000_000, 10),
+             ("k_rollout_argmin_stream", "qk21"): ("r04_close/valu/qk21.json", 1_000_000, 10),
+             ("k_rollout_generated", "rect+cum"): ("r04_close/valu/gen.json", 1_000_000, 10),
+             ("k_ft_leaves", "rect+rot"): ("r04_close/valu/ft.json", 451 ** 3, 3)}
 
 
 def valu_roofline(kernel, integrator, ms, n_cand, n_steps, note=None):
@@ -1093,7 +1094,29 @@ def bench_fulltree(args, wl, eng, rank, world, cpu):
     if args.dump_log and rank == 0:
         with open(args.dump_log, "w") as fh:
             json.dump(trace, fh)
-    flops = FT_FLOPS_PER_LEAF[args.integrator] * leaves / per_step / world   # per GPU
+    # The launches alone (mpc_fulltree_argmin: control table, leaves, selection)
+    # on the episode's last problem, back to back between HIP events on the
+    # current stream: the duration the rooflines divide by (the step above
+    # adds the drop-in's host work and the 200-B read-back).
+    from diplomjourney_amd.abi import MpcFulltreeProblem
+    from diplomjourney_amd.expansion import fulltree_argmin
+    feng, (fvg, fbg) = rmm._device()
+    fp = MpcFulltreeProblem(float(rmm.x), float(rmm.y), float(rmm.phi), float(rmm.x_t),
+                            float(rmm.y_t), float(rmm.x_0), float(rmm.y_0),
+                            float(_m.atan(rmm.x_t / rmm.y_t)), float(rmm.L), float(rmm.t),
+                            float(rmm.t + rmm.delta_t))
+    shard = (dist.get_rank(), world) if world > 1 else (0, 1)
+    for _ in range(3):
+        fulltree_argmin(feng, fp, fvg, fbg, float("inf"), args.integrator, *shard)
+    reps = 20
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    ev[0].record()
+    for _ in range(reps):
+        fulltree_argmin(feng, fp, fvg, fbg, float("inf"), args.integrator, *shard)
+    ev[1].record()
+    torch.cuda.synchronize()
+    launch_ms = ev[0].elapsed_time(ev[1]) / reps
+    flops = FT_FLOPS_PER_LEAF[args.integrator] * leaves / world / (launch_ms * 1e-3)   # per GPU
     out = {
         "metric": METRIC, "value": leaves * args.steps / elapsed, "unit": "leaves/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -1104,16 +1127,19 @@ def bench_fulltree(args, wl, eng, rank, world, cpu):
                    "parallelism": (f"leaf-sharded x{world}, all_gather(200 B)/step"
                                    if world > 1 else "single GPU")},
         "p50_ms": percentile(ms, 50),
+        "launch_ms": launch_ms,
+        "launch_note": "mpc_fulltree_argmin's three launches (k_ft_leaves ~96%), HIP events "
+                       "around 20 back-to-back calls on the last step's problem",
         "roofline": {"bound": "valu-fp64", "achieved": flops / 1e12,
                      "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": flops / 1e12 / FP64_VECTOR_PEAK_TFLOPS, "traffic": None,
                      "kernel": "k_ft_leaves",
-                     "note": "algorithmic fp64 ops per leaf as written (FT_FLOPS_PER_LEAF); "
-                             "leaves are generated from the index, no HBM stream"},
-        "roofline_valu": valu_roofline("k_ft_leaves", args.integrator, per_step * 1e3 * world,
+                     "note": "algorithmic fp64 ops per leaf as written (FT_FLOPS_PER_LEAF) over "
+                             "launch_ms; leaves are generated from the index, no HBM stream"},
+        "roofline_valu": valu_roofline("k_ft_leaves", args.integrator, launch_ms * world,
                                        leaves, 3,
-                                       note="counted fp64 ops of one MPC step (all leaves) over "
-                                            "the step's host time x ranks: a lower bound"),
+                                       note="counted fp64 ops of one MPC step (all leaves, PMC) "
+                                            "over launch_ms x ranks"),
         "cpu_baseline": cpu,
     }
     if rank == 0:

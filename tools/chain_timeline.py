@@ -25,7 +25,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 VAR = os.path.join(REPO, "tools", "var_timeline.so")
 NB = 2048 + 1
 B0 = ["entry", "records", "wave argmin", "block winner", "controls in LDS", "re-roll",
-      "advance", "update", "published"]
+      "advance", "update", "published", "adv-entry", "finishing", "pre-prepare", "prepared"]
 B0_BASE = 8 * NB   # block 0's stamps follow the tiles' (8 per block)
 TILE = ["entry", "DMAs issued", "final consts", "record stored"]
 
@@ -85,6 +85,12 @@ def build():
          f"  const mpc_candidate_t* g = wait_mailbox(S, mb, prev, world, n_steps);\n  {b0(3)}\n"),
         ("               kPubWords, publish_epoch);\n  emit_winner_tail",
          f"               kPubWords, publish_epoch);\n  {b0(8)}\n  emit_winner_tail"),
+        ("  EpisodeHead* S = &H;\n  S->steps_for_slowing -= 1;\n",
+         f"  {b0(9)}\n  EpisodeHead* S = &H;\n  S->steps_for_slowing -= 1;\n"),
+        ("  const double x_prev = S->x, y_prev = S->y;   // x_previous",
+         f"  {b0(10)}\n  const double x_prev = S->x, y_prev = S->y;   // x_previous"),
+        ("    episode_restart(c, *S);\n  }\n  episode_prepare(c, *S);\n}\n",
+         f"    episode_restart(c, *S);\n  }}\n  {b0(11)}\n  episode_prepare(c, *S);\n  {b0(12)}\n}}\n"),
         ("  L.status = status;\n  if (ended) {\n",
          f"  L.status = status;\n  {b0(6)}\n  if (ended) {{\n"),
         ("  if (blockIdx.x == 0) {\n    if (has_prev) {\n",

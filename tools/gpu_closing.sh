@@ -4,7 +4,7 @@
 # kernel stats of the default bench, PMC traffic + VALU passes of the chained
 # kernel, and the other workloads.  Everything lands under gpurun_out/$TAG;
 # every GPU step has its own time limit and the first failure ends the script.
-#   TAG=r03_close bash tools/gpu_closing.sh
+#   TAG=r04_close bash tools/gpu_closing.sh
 set -o pipefail
 OUT=gpurun_out/${TAG:-closing}
 mkdir -p $OUT
@@ -23,9 +23,14 @@ cp $OUT/rocprof/*/run_kernel_stats.csv $OUT/kernel_stats.csv 2>/dev/null || find
 step pmc 700 bash -c "TAG=${TAG:-closing}/pmc_chain ARGS='1000000 10 chain 20 4' bash tools/pmc.sh > $OUT/pmc_chain.log 2>&1"
 step pmc_sum 60 python3 tools/pmc_summary.py $OUT/pmc_chain $OUT/traffic_chain.json 160e6 k_episode_chain
 step valu 600 bash -c "TAG=${TAG:-closing}/valu bash tools/pmc_valu.sh > $OUT/valu.log 2>&1"
-for w in B D A; do
+step pmc_p2p 700 bash -c "TAG=${TAG:-closing}/pmc_p2p ARGS='1000000 10 p2p 20 4' bash tools/pmc.sh > $OUT/pmc_p2p.log 2>&1"
+step pmc_p2p_sum 60 python3 tools/pmc_summary.py $OUT/pmc_p2p $OUT/traffic_chain_p2p.json 160e6 "k_episode_chain<1, 2, 4" "k_episode_chain[p2p]"
+for w in B D A R F G E; do
   step bench_$w 300 bash -c "python bench.py --cpu-seconds 0 --no-second-pass --workload $w > $OUT/bench_$w.json 2> $OUT/bench_$w.err"
 done
 step bench_qk21 300 bash -c "python bench.py --cpu-seconds 0 --no-second-pass --integrator qk21 > $OUT/bench_qk21.json 2> $OUT/bench_qk21.err"
 step bench_exchange 300 bash -c "python bench.py --cpu-seconds 0 --no-second-pass --exchange > $OUT/bench_exchange.json 2> $OUT/bench_exchange.err"
+step bench_exchange_rccl 300 bash -c "python bench.py --cpu-seconds 0 --no-second-pass --exchange --exchange-mode rccl > $OUT/bench_exchange_rccl.json 2> $OUT/bench_exchange_rccl.err"
+step rocprof_p2p 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/rocprof_p2p -o run -- python3 bench.py --cpu-seconds 0 --no-second-pass --exchange
+find $OUT/rocprof_p2p -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats_p2p.csv \;
 echo "[closing] done" >&2

@@ -7,6 +7,8 @@ integ "chain": chained rect+cum episode steps instead (mpc_episode_chain_step,
 the bench default's launch: rollout of step k + completion of step k-1);
 "xchg": the exchange form of the chained step (mpc_episode_exchange_step +
 the RCCL all_gather, over a 1-rank nccl group: the N > 1 bench's launch);
+"p2p": the collective-free exchange form (mpc_episode_p2p_step, one rank: the
+N > 1 bench's launch);
 "generated": generated-controls episode steps (k_rollout_generated, rect+cum);
 "fulltree": config F's full-tree MPC steps (k_ft_leaves, S1 = 451, n_cand and
 n_steps ignored)."""
@@ -53,7 +55,7 @@ def main():
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
     pool = [eng.sample_controls(V, B, n, ns, 7 + i) for i in range(nb)]
-    if integ in ("chain", "xchg"):
+    if integ in ("chain", "xchg", "p2p"):
         from diplomjourney_amd.episode import DeviceEpisode
         xchg = integ == "xchg"
         if xchg:
@@ -64,8 +66,9 @@ def main():
                 port = s.getsockname()[1]
             dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
                                     world_size=1, device_id=torch.device("cuda", 0))
-        ep = DeviceEpisode(eng, n, ns, integrator="rect+cum", chain=True, exchange=xchg,
-                           log_capacity=8192)
+        p2p = integ == "p2p"
+        ep = DeviceEpisode(eng, n, ns, integrator="rect+cum", chain=True, exchange=xchg or p2p,
+                           log_capacity=8192, p2p=p2p)
         for i in range(reps):
             ep.step(controls=pool[i % nb])
         ep.flush()
