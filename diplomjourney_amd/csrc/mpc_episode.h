@@ -689,9 +689,15 @@ __device__ void collect_local_candidate(const Rec* __restrict__ part, int n_part
         }
         // consumed: untag both halves.  A replayed HIP graph repeats its
         // launches' epochs, so a record left tagged would pass for the
-        // replay's own before that launch's tile block stores it.
-        *const_cast<u64x2*>(reinterpret_cast<const u64x2*>(
-            reinterpret_cast<const char*>(part) + off[q])) = u64x2{0ull, 0ull};
+        // replay's own before that launch's tile block stores it.  Coherent
+        // (`sc1`) stores: a plain store could stay dirty in this XCD's L2 and
+        // be written back over a later record stored there by a block on
+        // another XCD with no kernel boundary in between (measured: a
+        // persistent multi-step variant of this collection timed out so).
+        uint64_t* h = reinterpret_cast<uint64_t*>(
+            const_cast<char*>(reinterpret_cast<const char*>(part)) + off[q]);
+        __hip_atomic_store(h, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(h + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   } else if (threadIdx.x == 0) {
@@ -1149,67 +1155,17 @@ constexpr int chain_waves() {
 // PL2 (wheelbase a power of two) is a template parameter, not a runtime
 // branch: with both rollout variants inlined the kernel held 119 VGPRs and
 // spilled 191 SGPRs; one variant per instantiation: 108-112 VGPRs, 81-86.
-template <int INTEG, int ROT, int MODE, bool PL2>
-__global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
-    EpisodeState* __restrict__ S, uint32_t epoch, const double* __restrict__ v,
-    const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part,
-    int has_prev, const Rec* __restrict__ part_prev, int n_part_prev,
-    const double* __restrict__ v_prev, const double* __restrict__ b_prev, int64_t index_base,
-    mpc_result_t* __restrict__ out_prev, const mpc_candidate_t* __restrict__ gathered,
-    int n_gathered, mpc_episode_config_t ecfg, mpc_episode_log_t* __restrict__ log, int cap,
-    uint32_t wait_tag) {
-  static_assert(ROT == kRotCum, "chained steps need the pose-independent recurrence");
-  if (blockIdx.x == 0) {
-    if (has_prev) {
-      // the completion of step k-1 publishes step k's constants itself, from
-      // its LDS copy of the updated head (store_update)
-      if constexpr (MODE == kChainP2P) {
-        // the previous launch's records -> this rank's candidate, posted to
-        // every mailbox; the world's awaited; selection and update.
-        // (`gathered` carries the mailbox, n_gathered the world size, wait_tag
-        // the previous step's epoch)
-        p2p_complete<INTEG, ROT>(ecfg, S, const_cast<mpc_candidate_t*>(gathered), n_gathered,
-                                 wait_tag, part_prev, n_part_prev, v_prev, b_prev, n_cand,
-                                 n_steps, index_base, out_prev, log, cap, epoch);
-      } else if constexpr (MODE == kChainFin) {
-        const Consts Kp = S->h.K;
-        const EpisodeHook hook{&S->h, log, cap, S->chain_pub, kPubWords, epoch};
-        // (block 0 never fills the control ring: its LDS holds the re-roll)
-        finalize_block<INTEG, ROT, true, kBlock, false>(part_prev, n_part_prev, Kp, v_prev,
-                                                        b_prev, n_cand, n_steps, index_base,
-                                                        S->h.incumbent, out_prev, ecfg, hook,
-                                                        ring_lds());
-      } else {
-        // overlapped exchange: the gathered candidates come from a collective
-        // that ran beside this launch — wait for its mark, stage them in LDS.
-        // P2P: wait for them in this rank's mailbox (`gathered` carries it,
-        // n_gathered the world size, wait_tag the previous step's epoch).
-        const mpc_candidate_t* g =
-            wait_tag ? wait_gathered(S, wait_tag, gathered, n_gathered) : gathered;
-        if (g)
-          advance_from_candidates<INTEG, ROT>(ecfg, S, g, n_gathered, out_prev, log, cap,
-                                              epoch, ring_lds());
-        else   // timed out (chain error 4): publish the unchanged head so no tile hangs
-          chain_publish(S, epoch);
-      }
-      __syncthreads();   // (the wheelbase check below reads the stored head)
-    } else {
-      chain_publish(S, epoch);   // no previous step: the head as reset / last updated
-    }
-    // The host picked PL2 from the caller's cfg; the tile blocks use the
-    // published head's wheelbase terms.  If those disagree (a cfg other than
-    // the one the state was reset with) every dphi would be formed with the
-    // wrong form: flag it (chain_error = 2) instead of returning wrong costs
-    // silently.  (chain_publish ended with a barrier after the head store.)
-    if (threadIdx.x == 0 && (S->h.K.L_pow2 != 0) != PL2) S->chain_error = 2u;
-    // kChainXchg passes the rank's candidate record in part_prev's slot (one
-    // kernel argument fewer: a further SGPR pair spilled a VGPR)
-    if constexpr (MODE == kChainXchg)
-      collect_local_candidate(part, gridDim.x - 1, epoch, v, b, n_cand, n_steps, index_base,
-                              reinterpret_cast<mpc_candidate_t*>(const_cast<Rec*>(part_prev)),
-                              &S->chain_error);
-    return;
-  }
+// The tile blocks of a chained launch (blocks 1..): stream this step's
+// controls through the LDS ring, speculating the step size until block 0 has
+// published the step's constants (see k_episode_chain), then the criterion
+// and the block's record into part[blockIdx.x - 1] (TAGGED: the exchange
+// form, whose records block 0 of the SAME launch collects).
+template <int INTEG, int ROT, bool PL2, bool TAGGED>
+__device__ __forceinline__ void chain_tiles(EpisodeState* __restrict__ S, uint32_t epoch,
+                                            const double* __restrict__ v,
+                                            const double* __restrict__ b, int64_t n_cand,
+                                            int n_steps, Rec* __restrict__ part, int has_prev,
+                                            const mpc_episode_config_t& ecfg) {
   constexpr int CPL = 2;
   __shared__ __attribute__((aligned(16))) uint32_t s_w[kPubWords];
   __shared__ uint32_t s_tag[kPubWords];
@@ -1319,11 +1275,76 @@ __global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
   }
   block_argmin<true>(best_k, best_i);   // (indices < n_cand < 2^31)
   if (threadIdx.x == 0) {
-    if constexpr (MODE == kChainXchg)
+    if constexpr (TAGGED)
       store_tagged_rec(&part[blockIdx.x - 1], best_k, best_i, epoch);
     else
       part[blockIdx.x - 1] = Rec{best_k, best_i};
   }
+}
+
+template <int INTEG, int ROT, int MODE, bool PL2>
+__global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
+    EpisodeState* __restrict__ S, uint32_t epoch, const double* __restrict__ v,
+    const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part,
+    int has_prev, const Rec* __restrict__ part_prev, int n_part_prev,
+    const double* __restrict__ v_prev, const double* __restrict__ b_prev, int64_t index_base,
+    mpc_result_t* __restrict__ out_prev, const mpc_candidate_t* __restrict__ gathered,
+    int n_gathered, mpc_episode_config_t ecfg, mpc_episode_log_t* __restrict__ log, int cap,
+    uint32_t wait_tag) {
+  static_assert(ROT == kRotCum, "chained steps need the pose-independent recurrence");
+  if (blockIdx.x == 0) {
+    if (has_prev) {
+      // the completion of step k-1 publishes step k's constants itself, from
+      // its LDS copy of the updated head (store_update)
+      if constexpr (MODE == kChainP2P) {
+        // the previous launch's records -> this rank's candidate, posted to
+        // every mailbox; the world's awaited; selection and update.
+        // (`gathered` carries the mailbox, n_gathered the world size, wait_tag
+        // the previous step's epoch)
+        p2p_complete<INTEG, ROT>(ecfg, S, const_cast<mpc_candidate_t*>(gathered), n_gathered,
+                                 wait_tag, part_prev, n_part_prev, v_prev, b_prev, n_cand,
+                                 n_steps, index_base, out_prev, log, cap, epoch);
+      } else if constexpr (MODE == kChainFin) {
+        const Consts Kp = S->h.K;
+        const EpisodeHook hook{&S->h, log, cap, S->chain_pub, kPubWords, epoch};
+        // (block 0 never fills the control ring: its LDS holds the re-roll)
+        finalize_block<INTEG, ROT, true, kBlock, false>(part_prev, n_part_prev, Kp, v_prev,
+                                                        b_prev, n_cand, n_steps, index_base,
+                                                        S->h.incumbent, out_prev, ecfg, hook,
+                                                        ring_lds());
+      } else {
+        // overlapped exchange: the gathered candidates come from a collective
+        // that ran beside this launch — wait for its mark, stage them in LDS.
+        // P2P: wait for them in this rank's mailbox (`gathered` carries it,
+        // n_gathered the world size, wait_tag the previous step's epoch).
+        const mpc_candidate_t* g =
+            wait_tag ? wait_gathered(S, wait_tag, gathered, n_gathered) : gathered;
+        if (g)
+          advance_from_candidates<INTEG, ROT>(ecfg, S, g, n_gathered, out_prev, log, cap,
+                                              epoch, ring_lds());
+        else   // timed out (chain error 4): publish the unchanged head so no tile hangs
+          chain_publish(S, epoch);
+      }
+      __syncthreads();   // (the wheelbase check below reads the stored head)
+    } else {
+      chain_publish(S, epoch);   // no previous step: the head as reset / last updated
+    }
+    // The host picked PL2 from the caller's cfg; the tile blocks use the
+    // published head's wheelbase terms.  If those disagree (a cfg other than
+    // the one the state was reset with) every dphi would be formed with the
+    // wrong form: flag it (chain_error = 2) instead of returning wrong costs
+    // silently.  (chain_publish ended with a barrier after the head store.)
+    if (threadIdx.x == 0 && (S->h.K.L_pow2 != 0) != PL2) S->chain_error = 2u;
+    // kChainXchg passes the rank's candidate record in part_prev's slot (one
+    // kernel argument fewer: a further SGPR pair spilled a VGPR)
+    if constexpr (MODE == kChainXchg)
+      collect_local_candidate(part, gridDim.x - 1, epoch, v, b, n_cand, n_steps, index_base,
+                              reinterpret_cast<mpc_candidate_t*>(const_cast<Rec*>(part_prev)),
+                              &S->chain_error);
+    return;
+  }
+  chain_tiles<INTEG, ROT, PL2, MODE == kChainXchg>(S, epoch, v, b, n_cand, n_steps, part,
+                                                   has_prev, ecfg);
 }
 
 }  // namespace mpc
