@@ -14,6 +14,9 @@ step() {   # step NAME SECONDS CMD...
   echo "[closing] $name" >&2
   timeout -k 10 $secs "$@" || { echo "[closing] $name failed ($?)" >&2; exit 1; }
 }
+# PART=1: tests, smoke, default bench + rocprof + PMC; PART=2: the rest (one
+# gpurun call each stays within its time limit); unset: both.
+if [ "${PART:-1}" = 1 ] || [ -z "$PART" ]; then
 step tests 900 bash -c "TAG=${TAG:-closing}/tests bash tools/gpu_tests.sh"
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 300 bash -c "python bench.py > $OUT/bench.json 2> $OUT/bench.err"
@@ -23,6 +26,8 @@ cp $OUT/rocprof/*/run_kernel_stats.csv $OUT/kernel_stats.csv 2>/dev/null || find
 step pmc 700 bash -c "TAG=${TAG:-closing}/pmc_chain ARGS='1000000 10 chain 20 4' bash tools/pmc.sh > $OUT/pmc_chain.log 2>&1"
 step pmc_sum 60 python3 tools/pmc_summary.py $OUT/pmc_chain $OUT/traffic_chain.json 160e6 k_episode_chain
 step valu 600 bash -c "TAG=${TAG:-closing}/valu bash tools/pmc_valu.sh > $OUT/valu.log 2>&1"
+fi
+if [ "${PART:-2}" = 2 ] || [ -z "$PART" ]; then
 step pmc_p2p 700 bash -c "TAG=${TAG:-closing}/pmc_p2p ARGS='1000000 10 p2p 20 4' bash tools/pmc.sh > $OUT/pmc_p2p.log 2>&1"
 step pmc_p2p_sum 60 python3 tools/pmc_summary.py $OUT/pmc_p2p $OUT/traffic_chain_p2p.json 160e6 "k_episode_chain<1, 2, 4" "k_episode_chain[p2p]"
 for w in B D A R F G E; do
@@ -33,4 +38,5 @@ step bench_exchange 300 bash -c "python bench.py --cpu-seconds 0 --no-second-pas
 step bench_exchange_rccl 300 bash -c "python bench.py --cpu-seconds 0 --no-second-pass --exchange --exchange-mode rccl > $OUT/bench_exchange_rccl.json 2> $OUT/bench_exchange_rccl.err"
 step rocprof_p2p 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/rocprof_p2p -o run -- python3 bench.py --cpu-seconds 0 --no-second-pass --exchange
 find $OUT/rocprof_p2p -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats_p2p.csv \;
+fi
 echo "[closing] done" >&2
