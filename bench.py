@@ -479,7 +479,10 @@ def main():
         # (the chained launch adds block 0's completion of the previous step)
         rollout_ms = kernel_pass(ep, pool)
     elif xchg_chain:
-        kern_ms = exchange_chain_pass(ep, pool)
+        # P2P: no collective between launches, so back-to-back launches
+        # between one pair of events (chain_pass); the all_gather form has its
+        # collective between two launches: a pair of events per launch
+        kern_ms = chain_pass(ep, pool) if p2p else exchange_chain_pass(ep, pool)
     elif inputs == "generated":
         pass   # events around the generated rollout + selection (no HBM roofline)
     elif hasattr(ep, "partials"):
@@ -873,7 +876,7 @@ XCHG_KERNEL = "k_episode_chain[exchange]"
 # chain's records + block 0's mailbox exchange)
 P2P_KERNEL = "k_episode_chain[p2p]"
 TRAFFIC_JSON = {"k_rollout_argmin_stream": "r03_traffic_stream.json",
-                "k_episode_chain": "r03_close/traffic_chain.json",
+                "k_episode_chain": "r04_close/traffic_chain.json",
                 XCHG_KERNEL: "r04/traffic_chain_xchg.json",
                 P2P_KERNEL: "r04_close/traffic_chain_p2p.json"}
 
