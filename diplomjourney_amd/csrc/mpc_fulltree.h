@@ -107,6 +107,7 @@ __device__ __forceinline__ void ft_leaves_body(const Consts& K, double atan_t,
   const int64_t n_waves = static_cast<int64_t>(gridDim.x) * kWaves;
   const int64_t n_pairs = s1 * s1;
   const int64_t n_chunks = (s1 + kFtChunk - 1) / kFtChunk;
+  double best_c = key_cost(best_k);   // (+inf: none yet)
   for (int64_t item = item_lo + wave; item < item_hi; item += n_waves) {
     const int64_t g = item / n_chunks;
     const int64_t c = item - g * n_chunks;
@@ -127,15 +128,19 @@ __device__ __forceinline__ void ft_leaves_body(const Consts& K, double atan_t,
     for (int64_t k2 = k2_lo; k2 < k2_hi; ++k2) {   // wave-uniform control
       const FtCtl u = ctl[k2];
       const FtState lf = ft_apply<INTEG, ROT>(l1, u, K);
-      const uint64_t kk = cost_key_nonneg(cost_fulltree(lf.x, lf.y, lf.ph, K, atan_t));
+      const double c = cost_fulltree(lf.x, lf.y, lf.ph, K, atan_t);
       // a lane's leaf indices only grow (items ascend, and so do (k0, k1) and
-      // k2 within them): strict < keeps its first minimum, as rec_less would
-      if (live && kk < best_k) {
-        best_k = kk;
+      // k2 within them): strict < keeps its first minimum, as rec_less would.
+      // Compared as doubles: the criterion is >= 0, where the double order is
+      // the cost keys' (+-0 equal, +inf and NaN never below a best), so the
+      // key is formed once per lane instead of per leaf.
+      if (live && c < best_c) {
+        best_c = c;
         best_i = j0 + k2;
       }
     }
   }
+  best_k = cost_key_nonneg(best_c);   // (+inf: ~0, no finite leaf)
 }
 
 template <int INTEG, bool ROT>
