@@ -884,10 +884,10 @@ TRAFFIC_JSON = {"k_rollout_argmin_stream": "r03_traffic_stream.json",
 # SQ_INSTS_VALU) of each kernel at the size it was measured on:
 # (kernel, integrator) -> (summary, candidates, horizon) — config C, or the
 # S1 = 451 full tree of config F (candidates = leaves)
-VALU_JSON = {("k_episode_chain", "rect+cum"): ("r04_close/valu/chain.json", 1_000_000, 10),
-             ("k_rollout_argmin_stream", "qk21"): ("r04_close/valu/qk21.json", 1_000_000, 10),
-             ("k_rollout_generated", "rect+cum"): ("r04_close/valu/gen.json", 1_000_000, 10),
-             ("k_ft_leaves", "rect+rot"): ("r04_close/valu/ft.json", 451 ** 3, 3)}
+VALU_JSON = {("k_episode_chain", "rect+cum"): ("r04_final/valu/chain.json", 1_000_000, 10),
+             ("k_rollout_argmin_stream", "qk21"): ("r04_final/valu/qk21.json", 1_000_000, 10),
+             ("k_rollout_generated", "rect+cum"): ("r04_final/valu/gen.json", 1_000_000, 10),
+             ("k_ft_leaves", "rect+rot"): ("r04_final/valu/ft.json", 451 ** 3, 3)}
 
 
 def valu_roofline(kernel, integrator, ms, n_cand, n_steps, note=None):

@@ -35,36 +35,13 @@ struct FtState {
   double x, y, ph, s, c;
 };
 
-// IEEE sqrt for the leaf criterion: the rsq + Newton sequence hipcc emits for
-// sqrt(double) (correctly rounded: the same bits as sqrt) without its input
-// scaling and special-case selects (13 instead of 18 VALU per leaf).  Exact
-// for 0 (selected) and for inputs >= 2^-767; below that (a leaf closer to
-// the target than 1e-115) and for +inf / NaN it returns NaN, which never wins
-// the strict < of the arg-min (+inf and NaN never do either).
-__device__ __forceinline__ double ft_sqrt(double x) {
-  const double y = __builtin_amdgcn_rsq(x);
-  double g = x * y, h = y * 0.5;
-  const double r = fma(-h, g, 0.5);
-  g = fma(g, r, g);
-  h = fma(h, r, h);
-  double d = fma(-g, g, x);
-  g = fma(d, h, g);
-  d = fma(-g, g, x);
-  g = fma(d, h, g);
-  return x == 0.0 ? 0.0 : g;
-}
-
 // criterion of run_math_model.py:82-86: 10000*dist_target (:64-65)
 // + 10*(arctan(x_t/y_t) - phi)^2 + 100*dist_line^2 (:53-61), in that order.
 MPC_HD __forceinline__ double cost_fulltree(double x, double y, double ph, const Consts& K,
                                            double atan_t) {
   const double a = atan_t - ph;
   const double ex = K.x_t - x, ey = K.y_t - y;
-#if defined(__HIP_DEVICE_COMPILE__)
-  const double dist_target = ft_sqrt(ex * ex + ey * ey);
-#else
-  const double dist_target = sqrt(ex * ex + ey * ey);
-#endif
+  const double dist_target = crit_sqrt(ex * ex + ey * ey);
   const double dl = fabs(K.A * x - K.B * y + K.C1 - K.C2) * K.inv_den;   // (mpc_device.h cost)
   const double d = (x == K.x_0 && y == K.y_0) ? 1000.0 : dl;
   return 10000.0 * dist_target + 10.0 * (a * a) + 100.0 * (d * d);
