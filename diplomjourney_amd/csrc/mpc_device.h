@@ -196,13 +196,16 @@ MPC_HD __forceinline__ void step_safe(double& x, double& y, double& ph, double v
 
 // IEEE sqrt for the criteria: on the device, the rsq + Newton sequence hipcc
 // emits for sqrt(double) (correctly rounded: the same bits as sqrt) without
-// its input scaling and special-case selects, 13 instead of 18 VALU.  Exact
-// for 0 (selected) and for every input >= 2^-767; below that (a terminal
+// its input scaling and special-case selects, 11 instead of 18 VALU.  Exact
+// for 0 and for every input >= 2^-767; below that (a terminal
 // state closer to the target than 1e-115) and for +inf / NaN it returns NaN,
 // which never wins the strict < of an arg-min (+inf and NaN never do either).
 MPC_HD __forceinline__ double crit_sqrt(double x) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  const double y = __builtin_amdgcn_rsq(x);
+  // (the estimate of max(x, 2^-767): x itself in the exact range; for x = 0 a
+  // finite estimate, so the sequence yields 0 exactly without a select; a NaN
+  // x still propagates through the products)
+  const double y = __builtin_amdgcn_rsq(fmax(x, 0x1p-767));
   double g = x * y, h = y * 0.5;
   const double r = fma(-h, g, 0.5);
   g = fma(g, r, g);
@@ -210,8 +213,7 @@ MPC_HD __forceinline__ double crit_sqrt(double x) {
   double d = fma(-g, g, x);
   g = fma(d, h, g);
   d = fma(-g, g, x);
-  g = fma(d, h, g);
-  return x == 0.0 ? 0.0 : g;
+  return fma(d, h, g);
 #else
   return sqrt(x);
 #endif

@@ -124,6 +124,8 @@ __device__ __forceinline__ void ft_leaves_body(const Consts& K, double atan_t,
 #ifndef MPC_FT_UNROLL
 #define MPC_FT_UNROLL 4   // k2 iterations interleaved (A/B: 1 -> 2 -> 4 = 353 -> 337 -> 335 us per config-F step)
 #endif
+    // the item's best k2 (32-bit; -1: none), its leaf index formed once per item
+    int32_t best_k2 = -1;
 #pragma unroll MPC_FT_UNROLL
     for (int64_t k2 = k2_lo; k2 < k2_hi; ++k2) {   // wave-uniform control
       const FtCtl u = ctl[k2];
@@ -134,11 +136,12 @@ __device__ __forceinline__ void ft_leaves_body(const Consts& K, double atan_t,
       // Compared as doubles: the criterion is >= 0, where the double order is
       // the cost keys' (+-0 equal, +inf and NaN never below a best), so the
       // key is formed once per lane instead of per leaf.
-      if (live && c < best_c) {
+      if (c < best_c) {
         best_c = c;
-        best_i = j0 + k2;
+        best_k2 = static_cast<int32_t>(k2);
       }
     }
+    if (best_k2 >= 0) best_i = j0 + best_k2;
   }
   best_k = cost_key_nonneg(best_c);   // (+inf: ~0, no finite leaf)
 }
