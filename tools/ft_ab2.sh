@@ -5,7 +5,7 @@
 set -o pipefail
 O=gpurun_out/${TAG:-ftab2}; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { echo "tests failed"; tail -20 $O/tests.log; exit 1; }
+timeout -k 10 500 python -u -m pytest ${TESTS:-tests} -x -q -m gpu --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { echo "tests failed"; tail -20 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 for v in tree prev tree2 prev2; do
   lib=""; case $v in prev*) lib=tools/var_ftprev.so;; esac
