@@ -876,9 +876,9 @@ XCHG_KERNEL = "k_episode_chain[exchange]"
 # chain's records + block 0's mailbox exchange)
 P2P_KERNEL = "k_episode_chain[p2p]"
 TRAFFIC_JSON = {"k_rollout_argmin_stream": "r03_traffic_stream.json",
-                "k_episode_chain": "r04_close/traffic_chain.json",
+                "k_episode_chain": "r04_final/close/traffic_chain.json",
                 XCHG_KERNEL: "r04/traffic_chain_xchg.json",
-                P2P_KERNEL: "r04_close/traffic_chain_p2p.json"}
+                P2P_KERNEL: "r04_final/close/traffic_chain_p2p.json"}
 
 # fp64 VALU counters (tools/pmc_valu.sh: SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F64,
 # SQ_INSTS_VALU) of each kernel at the size it was measured on:
