@@ -136,10 +136,10 @@ __device__ __forceinline__ void ft_leaves_body(const Consts& K, double atan_t,
       // Compared as doubles: the criterion is >= 0, where the double order is
       // the cost keys' (+-0 equal, +inf and NaN never below a best), so the
       // key is formed once per lane instead of per leaf.
-      if (c < best_c) {
-        best_c = c;
-        best_k2 = static_cast<int32_t>(k2);
-      }
+      // (c >= +0, never -0: the minimum of the doubles is the better one; a
+      // NaN c leaves best_c)
+      if (c < best_c) best_k2 = static_cast<int32_t>(k2);
+      best_c = fmin(best_c, c);
     }
     if (best_k2 >= 0) best_i = j0 + best_k2;
   }
