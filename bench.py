@@ -119,6 +119,14 @@ def parse():
                          "input); sampled: the device sampler regenerates them per step")
     ap.add_argument("--no-second-pass", action="store_true",
                     help="skip the comparison run with the other --inputs mode")
+    ap.add_argument("--no-config-d", action="store_true",
+                    help="workload C: skip the config-D sub-result (N=12, 1.25e6 candidates "
+                         "per GPU, the BASELINE multi-GPU config) measured in the same run")
+    ap.add_argument("--parity-steps", type=int, default=8,
+                    help="chained episode workloads: after the timed regions, log this many "
+                         "steps of a fresh episode and re-scan each on the host with the CPU "
+                         "oracle in the reference's arithmetic (qk21): the line's `parity` "
+                         "(0 = skip)")
     ap.add_argument("--fused", action="store_true",
                     help="one launch per step: the rollout's last block runs the selection "
                          "(mpc_episode_rollout) instead of a separate selection launch")
@@ -325,6 +333,27 @@ def bench_dropin(args, wl, eng, rank, world, cpu):
         print(json.dumps(out), flush=True)
 
 
+def visible_gpus():
+    """GPUs this process could use, counted without touching the GPU or
+    importing torch (the spawning parent stays GPU-free by construction):
+    the KFD topology's GPU nodes (gpu_id != 0), narrowed by the visibility
+    variables the HIP runtime honours.  0 when unknown (no check then)."""
+    import glob
+    n = 0
+    for f in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/gpu_id"):
+        try:
+            with open(f) as fh:
+                n += int(fh.read().strip() or 0) != 0
+        except (OSError, ValueError):
+            pass
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            ids = [x for x in v.split(",") if x.strip()]
+            n = min(n, len(ids)) if n else len(ids)
+    return n
+
+
 def spawn_ranks(args):
     """`python bench.py --gpus N` (N > 1) without a launcher: this process
     stays GPU-free (it never initialises HIP: device counting does not) and
@@ -338,8 +367,7 @@ def spawn_ranks(args):
     import subprocess
     n = args.gpus
     if args.dist_backend == "nccl":
-        import torch
-        have = torch.cuda.device_count()
+        have = visible_gpus()
         if have and n > have:
             print(f"bench: --gpus {n} needs {n} GPUs for RCCL ranks ({have} visible); "
                   "--dist-backend gloo rehearses more ranks than GPUs", file=sys.stderr)
@@ -416,6 +444,14 @@ def main():
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
         else:
             dist.init_process_group("gloo", rank=rank, world_size=world)
+    n_dev = max(1, torch.cuda.device_count())
+    if world > n_dev and args.workload in ("B", "C", "D"):
+        # a rehearsal: several ranks share each GPU — each launches on its own
+        # disjoint CU set, so that no rank's chained launch (tiles waiting for
+        # block 0, which waits for the peers) takes the CUs a peer needs
+        from diplomjourney_amd.episode import cu_share_stream
+        torch.cuda.set_stream(cu_share_stream(device, local_rank // n_dev,
+                                              -(-world // n_dev)))
     from diplomjourney_amd.expansion import Expansion
     eng = Expansion(device)
 
@@ -430,7 +466,45 @@ def main():
     if args.workload == "G":
         return bench_episodes(args, wl, eng, rank, world, cpu)
 
+    out, ep, pool = bench_episode(args, wl, eng, rank, world, device, cpu)
+    chain = getattr(ep, "chain", False) and args.inputs == "resident" and not args.host_loop
+    if chain and args.parity_steps > 0:
+        # checker, after every timed region: logged steps re-scanned on the
+        # host by the oracle in the reference's own arithmetic (qk21)
+        out["parity"] = parity_pass(args, eng, ep, pool, rank, world, device)
+    if args.workload == "C" and chain and not args.no_config_d:
+        # BASELINE config D (N=12, 1.25e6 candidates per GPU = 1e7 at 8) in
+        # the same run: at --gpus N the form the driver's scaling run measures
+        ep_form = getattr(ep, "p2p", False)
+        del pool
+        finish_episode(ep)
+        del ep
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        d_args = argparse.Namespace(**vars(args))
+        d_args.candidates_per_gpu = None
+        d_out, ep, pool = bench_episode(d_args, WORKLOADS["D"], eng, rank, world, device, None,
+                                        sub=True)
+        out["config_d"] = {k: d_out[k] for k in (
+            "value", "unit", "ms_per_step", "p50_ms", "chain_error", "exchange", "kernel_ms",
+            "roofline", "roofline_valu")}
+        out["config_d"]["config"] = {k: d_out["config"][k] for k in (
+            "workload", "n_steps", "candidates_per_gpu", "candidates_total", "launch",
+            "parallelism")}
+        assert getattr(ep, "p2p", False) == ep_form or world == 1, "config D changed form"
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    finish(ep, world > 1 or args.exchange)
+
+
+def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
+    """The episode workloads (B, C, D): returns (the JSON line's dict, the
+    DeviceEpisode, its resident pool).  sub: a secondary workload of the same
+    run (config D beside C) — no second input pass, no host latency pass."""
+    import torch
+    import torch.distributed as dist
     from diplomjourney_amd.episode import DeviceEpisode, Episode, cu_reserved_stream, percentile
+    group = None
     n_total = (args.candidates_per_gpu or wl["per_gpu"]) * world
     n_steps = wl["n_steps"]
     exchange = world > 1 or args.exchange
@@ -477,7 +551,7 @@ def main():
         kern_ms = chain_pass(ep, pool)
         # for comparison: the same controls through the rollout kernel alone
         # (the chained launch adds block 0's completion of the previous step)
-        rollout_ms = kernel_pass(ep, pool)
+        rollout_ms = None if sub else kernel_pass(ep, pool)
     elif xchg_chain:
         # P2P: no collective between launches, so back-to-back launches
         # between one pair of events (chain_pass); the all_gather form has its
@@ -489,10 +563,12 @@ def main():
         kern_ms = kernel_pass(ep, pool if pool is not None else
                               make_pool(eng, ep, n_steps, 4))
     other = generated = None
-    if not args.host_loop and not args.no_second_pass:
+    if not args.host_loop and not args.no_second_pass and not sub:
         # the other input mode, same episode machinery, for comparison
         other_pool = None if inputs == "resident" else make_pool(eng, ep, n_steps, args.steps)
-        r = run_steps(args, ep, other_pool, use_graph, world, device)
+        # (gloo collectives stage through the host: not capturable)
+        r = run_steps(args, ep, other_pool,
+                      use_graph and not (exchange and args.dist_backend == "gloo"), world, device)
         other = {"inputs": "sampled" if inputs == "resident" else "resident",
                  "value": n_total * args.steps / r["elapsed"],
                  "ms_per_step": r["elapsed"] / args.steps * 1e3, "p50_ms": r["p50_ms"]}
@@ -511,7 +587,7 @@ def main():
                              note="over the whole step (generated rollout + selection): a "
                                   "lower bound of the rollout kernel's rate")}
     host_ms = None
-    if not args.host_loop and not exchange:
+    if not args.host_loop and not exchange and not sub:
         host_ms = host_latency_pass(ep, pool)
     elapsed = main_run["elapsed"]
     chain_step = getattr(ep, "chain", False) and inputs == "resident"
@@ -612,9 +688,106 @@ def main():
         out["roofline"]["stream_ceiling_ms"] = ceil_ms
         out["roofline"]["frac_of_stream_ceiling"] = achieved / ceil
         out["roofline"]["valu"] = valu_share(args.traffic_json, kernel, bytes_launch, kern_ms)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1 or args.exchange:
+    return out, ep, pool
+
+
+def parity_pass(args, eng, ep, pool, rank, world, device):
+    """CHECKER, run after every timed region and never timed: the identity of
+    the bench's chosen controls with the reference's arithmetic at full size
+    (SURVEY §7 hard part 2).  A fresh episode of the bench's own form (same
+    shard, step form and exchange) logs --parity-steps chained steps over the
+    first resident batches; every step's problem is rebuilt on the host from
+    the log (episode.logged_step_problems) and each rank re-scans its shard
+    with the CPU oracle in qk21 mode (scipy quad's 21-point Kronrod sums, glibc
+    trig, the reference's operation order: oracle/mpc_oracle.c, pinned bitwise
+    to the reference's own outputs); the ranks' lexicographic (cost, index)
+    minima give the oracle's global winner.  identity_rate: the share of
+    steps whose logged winner is the oracle's; for mismatches the oracle's own
+    relative cost gap between the two (max_rel_dcost_mismatch); and the
+    largest relative difference between the logged cost and the oracle's cost
+    of the same candidate (the two arithmetics' noise)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    from diplomjourney_amd.episode import DeviceEpisode, logged_step_problems
+    K = min(args.parity_steps, len(pool))
+    t_start = time.perf_counter()
+    fresh = DeviceEpisode(eng, ep.n_total, ep.n_steps, rank=rank, world=world,
+                          integrator=ep.integrator, group=ep.group, log_capacity=max(64, K),
+                          exchange=ep.exchange, chain=True, p2p=getattr(ep, "p2p", False))
+    for i in range(K):
+        fresh.step(controls=pool[i])
+    fresh.flush()
+    log = fresh.read_log()
+    probs = logged_step_problems(log, fresh.cfg)
+    try:
+        threads = max(1, min(16, len(os.sched_getaffinity(0)) // max(1, world)))
+    except AttributeError:
+        threads = 4
+    rows = np.full((K, 4), np.nan)     # best cost, best global index, cost at the logged index
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        futs = []
+        for i in range(K):
+            vh, bh = (a.cpu().numpy() for a in pool[i])
+            futs.append(ex.submit(O.rollout_argmin, probs[i][0], vh, bh, index_base=fresh.lo,
+                                  incumbent=probs[i][1], integ="qk21", want_costs=True))
+        for i, f in enumerate(futs):
+            ref, costs, _ = f.result()
+            rows[i, 0], rows[i, 1] = ref.cost, ref.index
+            j = log[i].index - fresh.lo
+            if 0 <= j < fresh.n_local:
+                rows[i, 2] = costs[j]
+            rows[i, 3] = float(ref.found)
+    finish_episode(fresh)
+    if world > 1:
+        on_dev = dist.get_backend() == "nccl"
+        t = torch.from_numpy(rows).to(device if on_dev else "cpu")
+        allr = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(allr, t)
+        per = np.stack([a.cpu().numpy() for a in allr])          # [world, K, 4]
+    else:
+        per = rows[None]
+    same, gaps, noise = 0, [], 0.0
+    for i in range(K):
+        best = min(range(world), key=lambda r: (per[r, i, 0], per[r, i, 1]))
+        c_best, i_best = per[best, i, 0], int(per[best, i, 1])
+        c_logged = np.nanmin(per[:, i, 2])       # the one rank holding the logged index
+        if log[i].index == i_best:
+            same += 1
+            noise = max(noise, abs(log[i].cost - c_best) / abs(c_best))
+        else:
+            gaps.append(float(abs(c_logged - c_best) / abs(c_best)))
+    return {"steps": K, "identity_rate": same / K, "mismatches": len(gaps),
+            "max_rel_dcost_mismatch": max(gaps) if gaps else 0.0,
+            "max_rel_cost_diff_identical": noise,
+            "oracle": "qk21 (the reference's scipy quad arithmetic), oracle/mpc_oracle.c",
+            "threads_per_rank": threads, "check_s": time.perf_counter() - t_start,
+            "note": "checker after the timed regions: a fresh episode of the bench's step "
+                    "form over the first resident batches, each step re-scanned in full on "
+                    "the host; not part of any timed value"}
+
+
+def finish_episode(ep):
+    """An episode done with: drain it and release its mailbox (every rank)."""
+    import torch
+    import torch.distributed as dist
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.barrier()       # no peer still stores into this rank's mailbox
+    close = getattr(ep, "close", None)
+    if close:
+        close()
+    torch.cuda.synchronize()
+
+
+def finish(ep, have_group):
+    """Drain everything this run enqueued (peer stores, a side stream's last
+    collective), release the episode's mailbox, then the process group — so
+    nothing is in flight when the runtime tears down at exit."""
+    import torch.distributed as dist
+    finish_episode(ep)
+    if have_group and dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -680,15 +853,9 @@ def valu_share(traffic_json, kernel, bytes_launch, kern_ms):
     the fp64 issue rate they take: 4 cycles per wave-instruction on each of the
     1024 SIMDs at 2.4 GHz (78.6 TFLOP/s of fp64 FMA); integer and fp32 VALU
     instructions are counted as fp64 ones, so the share is an upper bound."""
-    path = traffic_json or (os.path.join(REPO, "profiles", TRAFFIC_JSON[kernel])
-                            if kernel in TRAFFIC_JSON else None)
-    if not path or not os.path.exists(path):
-        return None
-    with open(path) as fh:
-        t = json.load(fh)
-    insts = t.get("counters_median_per_launch", {}).get("SQ_INSTS_VALU")
-    if (insts is None or t.get("kernel", kernel) != kernel
-            or abs(t.get("algorithmic_bytes_per_launch", -1) - bytes_launch) >= 1):
+    t, path = traffic_summary(traffic_json, kernel, bytes_launch)
+    insts = t.get("counters_median_per_launch", {}).get("SQ_INSTS_VALU") if t else None
+    if insts is None:
         return None
     return {"wave_insts_per_launch": insts, "source": os.path.relpath(path, REPO),
             "fp64_issue_share": insts * 4.0 / (1024 * 2.4e9 * kern_ms * 1e-3)}
@@ -875,10 +1042,30 @@ XCHG_KERNEL = "k_episode_chain[exchange]"
 # ... and its P2P form (k_episode_chain<..., kChainP2P, ...>: the one-GPU
 # chain's records + block 0's mailbox exchange)
 P2P_KERNEL = "k_episode_chain[p2p]"
-TRAFFIC_JSON = {"k_rollout_argmin_stream": "r03_traffic_stream.json",
-                "k_episode_chain": "r04_final/close/traffic_chain.json",
-                XCHG_KERNEL: "r04/traffic_chain_xchg.json",
-                P2P_KERNEL: "r04_final/close/traffic_chain_p2p.json"}
+# committed PMC summaries (tools/pmc.sh + tools/pmc_summary.py), per kernel
+# one per measured size; the one whose algorithmic bytes match is used
+TRAFFIC_JSON = {"k_rollout_argmin_stream": ["r03_traffic_stream.json"],
+                "k_episode_chain": ["r04_final/close/traffic_chain.json",
+                                    "r05/traffic_chain_D.json"],
+                XCHG_KERNEL: ["r04/traffic_chain_xchg.json"],
+                P2P_KERNEL: ["r04_final/close/traffic_chain_p2p.json",
+                             "r05/traffic_chain_p2p_D.json"]}
+
+
+def traffic_summary(traffic_json, kernel, bytes_launch):
+    """(summary dict, path) of the PMC summary measured on this kernel at this
+    algorithmic size (traffic_json: an explicit file), else (None, None)."""
+    paths = ([traffic_json] if traffic_json else
+             [os.path.join(REPO, "profiles", p) for p in TRAFFIC_JSON.get(kernel, [])])
+    for path in paths:
+        if not path or not os.path.exists(path):
+            continue
+        with open(path) as fh:
+            t = json.load(fh)
+        if (abs(t.get("algorithmic_bytes_per_launch", -1) - bytes_launch) < 1
+                and t.get("kernel", kernel) == kernel):
+            return t, path
+    return None, None
 
 # fp64 VALU counters (tools/pmc_valu.sh: SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F64,
 # SQ_INSTS_VALU) of each kernel at the size it was measured on:
@@ -945,14 +1132,9 @@ def roofline(achieved, bytes_launch, traffic_json, kernel="k_rollout_argmin_stre
     """traffic: HBM bytes per launch from the committed PMC summary, used only
     when it was measured on the same kernel at the same algorithmic size."""
     traffic, src = None, None
-    if traffic_json is None and kernel in TRAFFIC_JSON:
-        traffic_json = os.path.join(REPO, "profiles", TRAFFIC_JSON[kernel])
-    if traffic_json and os.path.exists(traffic_json):
-        with open(traffic_json) as fh:
-            t = json.load(fh)
-        if (abs(t.get("algorithmic_bytes_per_launch", -1) - bytes_launch) < 1
-                and t.get("kernel", kernel) == kernel):
-            traffic, src = t.get("hbm_bytes_per_launch"), os.path.relpath(traffic_json, REPO)
+    t, path = traffic_summary(traffic_json, kernel, bytes_launch)
+    if t:
+        traffic, src = t.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
             "kernel": kernel, "algorithmic_bytes_per_launch": bytes_launch}

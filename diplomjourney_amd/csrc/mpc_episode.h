@@ -22,7 +22,43 @@
 namespace mpc {
 
 constexpr int kEpMaxGrid = 64;
-constexpr uint32_t kChainSpinLimit = 1u << 17;   // bounded device waits: x ~1-2k cycles, ~0.1 s
+
+// Bounded device waits, measured on the GPU's constant-rate wall clock
+// (wall_clock64: s_memrealtime, 100 MHz on gfx950) rather than in poll passes,
+// so that waits of different loops compare: a wait that runs out sets
+// chain_error instead of hanging the GPU.
+//   kChainWaitTicks   one GPU: a chained launch's tiles wait for block 0,
+//                     which waits for nothing outside the launch
+//   kPeerWaitTicks    block 0 waits for other ranks (P2P mailbox, error 5) or
+//                     for a collective beside the launch (error 4); ranks are
+//                     not barrier-aligned between steps, so a peer may start
+//                     the same step a host hiccup later
+//   kXchgWaitTicks    an exchange launch's tiles wait for THAT block 0: longer
+//                     than its peer wait, so a late peer surfaces as block 0's
+//                     error (or not at all), never as tiles scoring the step on
+//                     speculated constants (error 1)
+constexpr uint64_t kWallHz = 100000000ull;
+constexpr uint64_t kChainWaitTicks = kWallHz / 5;        // 0.2 s
+constexpr uint64_t kPeerWaitTicks = 2 * kWallHz;         // 2 s
+constexpr uint64_t kXchgWaitTicks = 3 * kWallHz;         // 3 s
+static_assert(kXchgWaitTicks > kPeerWaitTicks, "tiles outwait their block 0");
+
+// 32-bit deadlines (one register; the low word wraps after 42 s, far beyond
+// any budget here, and the comparison is wrap-safe)
+__device__ __forceinline__ uint32_t wall_deadline(uint64_t ticks) {
+  return static_cast<uint32_t>(wall_clock64()) + static_cast<uint32_t>(ticks);
+}
+__device__ __forceinline__ bool wall_passed(uint32_t deadline) {
+  return static_cast<int32_t>(static_cast<uint32_t>(wall_clock64()) - deadline) > 0;
+}
+// Block-wide (all threads, same pass): has the deadline passed?  Thread 0's
+// clock decides, so every wave leaves a __syncthreads_* poll on the same pass.
+__device__ __forceinline__ bool block_wall_passed(uint32_t deadline) {
+  // (readfirstlane: the compiler sees a uniform value, so a loop that leaves
+  // on it stays uniform and its loop-invariant pointers stay in SGPRs)
+  return __builtin_amdgcn_readfirstlane(
+             __syncthreads_or(threadIdx.x == 0 && wall_passed(deadline))) != 0;
+}
 constexpr int kConstsWords = static_cast<int>(sizeof(Consts) / 4);
 constexpr int kPubWords = kConstsWords + 2;   // Consts, then t
 static_assert(sizeof(Consts) % 4 == 0 && kPubWords <= 64, "published words: one wave");
@@ -37,6 +73,12 @@ struct EpisodeState {
   double grid_b[kEpMaxGrid];
   uint32_t done;       // blocks of the running fused launch that have finished
   uint32_t chain_error;   // a chained step's wait timed out (k_episode_chain)
+  // P2P exchange: completions so far; completion c uses mailbox slot c & 1.
+  // Counted on the device (every rank completes the same steps), not taken
+  // from the launch's epoch: a replayed HIP graph repeats its epochs, and a
+  // captured sequence of odd length would start its next replay in the slot
+  // its flush was still reading on a slower rank.
+  uint32_t p2p_seq;
   // Constants published by a chained launch's block 0 (k_episode_chain): the
   // dwords of the step's Consts and of t, each in a 64-bit word tagged with
   // the launch's epoch ((dword << 32) | epoch), so one coherent load per word
@@ -120,6 +162,7 @@ __global__ void k_episode_reset(mpc_episode_config_t c, EpisodeState* __restrict
   S->h = H;
   S->done = 0u;
   S->chain_error = 0u;
+  S->p2p_seq = 0u;
   for (int q = 0; q < kPubWords; ++q) S->chain_pub[q] = 0ull;
   S->gathered_tag = 0ull;
 }
@@ -661,6 +704,9 @@ __device__ void collect_local_candidate(const Rec* __restrict__ part, int n_part
   }
   bool timed_out = false;
   const uint32_t tag = rec_tag(epoch);
+  // Bounded in passes (~1-2 us each: 2^20 passes, >= 1 s; the tiles may share
+  // the GPU with other processes' launches).  A clock check here (a second
+  // block-wide barrier per check) kept 52 B of VGPR spills in this form.
   for (uint32_t it = 0;; ++it) {
     load8_rec_sc1_sbase(part, off, r);
     bool ok = true;
@@ -668,7 +714,7 @@ __device__ void collect_local_candidate(const Rec* __restrict__ part, int n_part
     for (int q = 0; q < 8; ++q)
       if (threadIdx.x + q * kBlock < n_part) ok = ok && tagged_rec_fresh(r[q], tag);
     if (__syncthreads_and(ok)) break;
-    if (it >= kChainSpinLimit) {   // uniform: every thread counts the same passes
+    if (it >= (1u << 20)) {   // uniform: every thread counts the same passes
       timed_out = true;
       break;
     }
@@ -747,15 +793,17 @@ static_assert(kXchgLdsRanks * sizeof(mpc_candidate_t) + sizeof(EmitLds) <= sizeo
 __device__ const mpc_candidate_t* wait_gathered(EpisodeState* S, uint32_t tag,
                                                 const mpc_candidate_t* __restrict__ g, int n) {
   __shared__ int s_ok;
-  if (threadIdx.x < 64) {
+  if (threadIdx.x < 64) {   // one wave: its clock reads are uniform
     bool ok = false;
-    for (uint32_t it = 0; it < kChainSpinLimit; ++it) {
+    const uint32_t deadline = wall_deadline(kPeerWaitTicks);
+    for (;;) {
       const uint64_t w = __hip_atomic_load(&S->gathered_tag, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
       if (static_cast<uint32_t>(w) == tag) {
         ok = true;
         break;
       }
+      if (wall_passed(deadline)) break;
       __builtin_amdgcn_s_sleep(2);
     }
     if (threadIdx.x == 0) {
@@ -887,7 +935,8 @@ __device__ __forceinline__ bool chain_read(const EpisodeState* S, uint32_t epoch
 // GPU's loads see).  Block 0 of rank q's launch with epoch e+1 — the launch
 // that completes step e — reduces step e's block records (the previous
 // launch's, stream-ordered: plain loads) into q's candidate and stores it into
-// slot e&1, row q, of EVERY rank's mailbox (its own included); it then waits
+// slot c&1 (c = the episode's P2P completions so far, EpisodeState::p2p_seq),
+// row q, of EVERY rank's mailbox (its own included); it then waits
 // until the world's candidates of step e are complete in its own mailbox,
 // stages them in LDS, clears them, selects the global winner and updates the
 // episode.  The tile blocks meanwhile stream step e+1 (its constants are
@@ -902,9 +951,11 @@ __device__ __forceinline__ bool chain_read(const EpisodeState* S, uint32_t epoch
 // reader polls the granules themselves.  Only the words a step needs move:
 // cost, index, (n_steps, reserved), v[0..n_steps), beta[0..n_steps).
 // A consumed granule is zeroed by its reader.  Two slots suffice: rank q
-// writes slot e&1 again only for step e+2, after it has read every rank's
-// step-(e+1) candidate — each posted in a launch that began after the launch
-// whose zeroing stores had completed (a kernel boundary).
+// writes slot c&1 again only for completion c+2, after it has read every
+// rank's completion-(c+1) candidate — each posted in a launch that began after
+// the launch whose zeroing stores had completed (a kernel boundary).  This
+// holds across graph replays whatever the captured length (the count lives on
+// the device; the epochs only tag the granules).
 //   layout: MailHdr (the peers' mailbox pointers as mapped in this process,
 //           this rank, the world size, ping words), then granule
 //           [2][world][kCandWords] of 16 B
@@ -921,8 +972,7 @@ static_assert(sizeof(mpc_candidate_t) % 8 == 0, "candidates move as 8-B words");
 static_assert(offsetof(mpc_candidate_t, v) == 24 && offsetof(mpc_candidate_t, beta) ==
                   24 + 8 * MPC_MAX_STEPS, "candidate word map (cand_word)");
 // Peers' launches are not stream-ordered with this one: a rank may start its
-// step a host-side hiccup later.  ~1 s before chain error 5.
-constexpr uint32_t kP2PSpinLimit = 1u << 24;
+// step a host-side hiccup later.  kPeerWaitTicks (2 s) before chain error 5.
 
 __host__ __device__ inline size_t mailbox_bytes(int world) {
   return kMailHdrBytes + 2 * static_cast<size_t>(world) * kMailRecBytes;
@@ -1012,8 +1062,7 @@ __device__ void records_candidate(const Rec* __restrict__ part, int n_part,
 // to every rank's mailbox as tagged granules (16-B `sc0 sc1` stores; nothing
 // waits for them).
 __device__ void post_candidate(const uint64_t* s_peers, int rank, int world, uint32_t epoch,
-                               int n_steps, const mpc_candidate_t* cand) {
-  const uint32_t slot = epoch & 1u;
+                               uint32_t slot, int n_steps, const mpc_candidate_t* cand) {
   const uint64_t tag = rec_tag(epoch);
   const int words = 3 + 2 * n_steps;
   __syncthreads();   // the candidate is complete in LDS
@@ -1036,11 +1085,12 @@ __device__ void post_candidate(const uint64_t* s_peers, int rank, int world, uin
 // into LDS (cand_lds) and zero the granules.  Returns the LDS copy, or nullptr
 // on a timeout.
 __device__ const mpc_candidate_t* wait_mailbox(EpisodeState* S, void* mb, uint32_t epoch,
-                                               int world, int n_steps) {
-  const uint32_t slot = epoch & 1u;
+                                               uint32_t slot, int world, int n_steps,
+                                               uint64_t ticks) {
   const uint32_t tag = rec_tag(epoch);
   const int words = 3 + 2 * n_steps, total = world * words;
   mpc_candidate_t* dst = cand_lds();
+  const uint32_t deadline = wall_deadline(ticks);
   uint32_t it = 0;
   // one granule per thread and pass (world * words <= 256 in one pass: up to
   // 11 ranks at N = 10); a later chunk is polled after the earlier is in
@@ -1058,8 +1108,9 @@ __device__ const mpc_candidate_t* wait_mailbox(EpisodeState* S, void* mb, uint32
         g.y = __hip_atomic_load(h + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         ok = tagged_rec_fresh(g, tag);
       }
-      if (__syncthreads_and(ok)) break;   // uniform: every thread counts the same passes
-      if (it >= kP2PSpinLimit) {
+      if (__syncthreads_and(ok)) break;
+      // uniform: every thread counts the same passes, thread 0's clock decides
+      if ((it & 63) == 63 && block_wall_passed(deadline)) {
         if (threadIdx.x == 0) S->chain_error = 5u;
         return nullptr;
       }
@@ -1091,15 +1142,27 @@ __device__ void p2p_complete(const mpc_episode_config_t& c, EpisodeState* S, voi
   __shared__ uint64_t s_peers[kMailMaxRanks];
   __shared__ int s_rank;
   const MailHdr* hdr = static_cast<const MailHdr*>(mb);
+  __shared__ uint32_t s_err, s_seq;
   const uint64_t my_peer = static_cast<int>(threadIdx.x) < world ? hdr->peers[threadIdx.x] : 0;
   const int my_rank = threadIdx.x == 0 ? hdr->rank : 0;
+  // an earlier step of this episode already timed out (a peer gone): fail
+  // fast instead of waiting the full budget again on every later step
+  const uint32_t prior_err = threadIdx.x == 0 ? S->chain_error : 0u;
+  const uint32_t seq = threadIdx.x == 0 ? S->p2p_seq : 0u;
   mpc_candidate_t* lc = cand_lds();
   records_candidate(part_prev, n_part_prev, v_prev, b_prev, n_cand, n_steps, index_base, lc);
   if (static_cast<int>(threadIdx.x) < world) s_peers[threadIdx.x] = my_peer;
-  if (threadIdx.x == 0) s_rank = my_rank;
+  if (threadIdx.x == 0) {
+    s_rank = my_rank;
+    s_err = prior_err;
+    s_seq = seq;
+  }
   __syncthreads();
-  post_candidate(s_peers, s_rank, world, prev, n_steps, lc);
-  const mpc_candidate_t* g = wait_mailbox(S, mb, prev, world, n_steps);
+  const uint32_t slot = s_seq & 1u;
+  post_candidate(s_peers, s_rank, world, prev, slot, n_steps, lc);
+  const mpc_candidate_t* g =
+      wait_mailbox(S, mb, prev, slot, world, n_steps, s_err ? 0ull : kPeerWaitTicks);
+  if (threadIdx.x == 0) S->p2p_seq = s_seq + 1u;   // read by the next launch
   if (g) {
     advance_from_candidates<INTEG, ROT>(c, S, g, world, out_prev, log, cap, publish_epoch,
                                         ring_lds());
@@ -1122,7 +1185,8 @@ __global__ __launch_bounds__(64) void k_mailbox_ping(void* mb, uint32_t tag, int
     __hip_atomic_store(&static_cast<MailHdr*>(reinterpret_cast<void*>(hdr->peers[r]))->ping[rank],
                        static_cast<uint64_t>(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   bool seen = r >= world;
-  for (uint32_t it = 0; it < kChainSpinLimit && __ballot(!seen) != 0; ++it) {
+  const uint32_t deadline = wall_deadline(kPeerWaitTicks);   // one wave: uniform clock
+  while (__ballot(!seen) != 0 && !wall_passed(deadline)) {
     if (!seen)
       seen = __hip_atomic_load(&hdr->ping[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ==
              static_cast<uint64_t>(tag);
@@ -1159,8 +1223,10 @@ constexpr int chain_waves() {
 // controls through the LDS ring, speculating the step size until block 0 has
 // published the step's constants (see k_episode_chain), then the criterion
 // and the block's record into part[blockIdx.x - 1] (TAGGED: the exchange
-// form, whose records block 0 of the SAME launch collects).
-template <int INTEG, int ROT, bool PL2, bool TAGGED>
+// form, whose records block 0 of the SAME launch collects).  WAIT_TICKS bounds
+// the wait for block 0's constants (kChainWaitTicks on one GPU,
+// kXchgWaitTicks when block 0 itself waits for peers or a collective).
+template <int INTEG, int ROT, bool PL2, bool TAGGED, uint64_t WAIT_TICKS>
 __device__ __forceinline__ void chain_tiles(EpisodeState* __restrict__ S, uint32_t epoch,
                                             const double* __restrict__ v,
                                             const double* __restrict__ b, int64_t n_cand,
@@ -1237,8 +1303,9 @@ __device__ __forceinline__ void chain_tiles(EpisodeState* __restrict__ S, uint32
           fin = __ballot(!ok) == 0;
           if (fin && threadIdx.x < kPubWords) s_w[threadIdx.x] = static_cast<uint32_t>(w_pre >> 32);
         }
-        uint32_t it = 0;
-        while (!fin && !(fin = chain_read(S, epoch, s_w, s_tag)) && ++it < kChainSpinLimit)
+        // (wave 0 only: its clock reads are uniform)
+        const uint32_t deadline = wall_deadline(WAIT_TICKS);
+        while (!fin && !(fin = chain_read(S, epoch, s_w, s_tag)) && !wall_passed(deadline))
           __builtin_amdgcn_s_sleep(4);
         if (!fin && threadIdx.x == 0) S->chain_error = 1u;
       }
@@ -1343,8 +1410,9 @@ __global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
                               &S->chain_error);
     return;
   }
-  chain_tiles<INTEG, ROT, PL2, MODE == kChainXchg>(S, epoch, v, b, n_cand, n_steps, part,
-                                                   has_prev, ecfg);
+  chain_tiles<INTEG, ROT, PL2, MODE == kChainXchg,
+              MODE == kChainFin ? kChainWaitTicks : kXchgWaitTicks>(S, epoch, v, b, n_cand,
+                                                                    n_steps, part, has_prev, ecfg);
 }
 
 }  // namespace mpc

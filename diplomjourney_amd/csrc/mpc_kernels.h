@@ -916,6 +916,13 @@ __device__ __forceinline__ void load8_rec_sc1(const Rec* const (&p)[8], u64x2 (&
 // its records with these, and its register peak is the kernel's).
 __device__ __forceinline__ void load8_rec_sc1_sbase(const Rec* base, const uint32_t (&o)[8],
                                                     u64x2 (&r)[8]) {
+  // (the base through readfirstlane: uniform for the compiler whatever loop
+  // the call sits in, so the "s" operand is an SGPR pair)
+  const uint64_t ab = reinterpret_cast<uint64_t>(base);
+  base = reinterpret_cast<const Rec*>(
+      (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+           static_cast<int>(ab >> 32)))) << 32) |
+      static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(ab))));
   asm volatile(
       "s_nop 4\n\t"   // VALU-written SGPR -> VMEM: see glds_pair
       "global_load_dwordx4 %0, %8, %16 sc1\n\t"

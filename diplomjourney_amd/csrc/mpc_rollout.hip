@@ -648,13 +648,19 @@ int mpc_episode_exchange_step2(const mpc_episode_config_t* cfg, void* state, uin
 int mpc_stream_create_cu_reserved(int32_t reserved_per_xcd, mpc_stream_t* stream) {
   if (!stream || reserved_per_xcd < 0 || reserved_per_xcd > 8) return MPC_ERR_ARG;
   int dev = 0, ncu = 0;
+  hipDeviceProp_t prop;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      ncu < 16)
+      hipGetDeviceProperties(&prop, dev) != hipSuccess)
     return MPC_ERR_HIP;
   // Logical CU i of a stream's CU mask sits on XCD i % 8: bits 0-7 are CU 0
-  // of XCDs 0-7 (measured, tools/micro/cumask.hip), so clearing the first
-  // 8 * r bits leaves r CUs of every XCD to other streams.
+  // of XCDs 0-7 (measured on an MI355X in SPX mode, tools/micro/cumask.hip),
+  // so clearing the first 8 * r bits leaves r CUs of every XCD to other
+  // streams.  That layout was measured on one part only: any other device
+  // (another architecture, or a partition mode with fewer XCDs / CUs) is
+  // refused rather than given a mask that reserves the wrong CUs.
+  if (ncu != 256 || strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return MPC_ERR_UNSUPPORTED;
   uint32_t mask[16];
   const int words = (ncu + 31) / 32;
   if (words > 16) return MPC_ERR_UNSUPPORTED;
@@ -663,6 +669,26 @@ int mpc_stream_create_cu_reserved(int32_t reserved_per_xcd, mpc_stream_t* stream
   hipStream_t st = nullptr;
   if (hipExtStreamCreateWithCUMask(&st, static_cast<uint32_t>(words), mask) != hipSuccess)
     return MPC_ERR_HIP;
+  *stream = reinterpret_cast<mpc_stream_t>(st);
+  return MPC_OK;
+}
+
+int mpc_stream_create_cu_share(int32_t part, int32_t parts, mpc_stream_t* stream) {
+  if (!stream || parts < 1 || parts > 32 || part < 0 || part >= parts) return MPC_ERR_ARG;
+  int dev = 0, ncu = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipGetDeviceProperties(&prop, dev) != hipSuccess)
+    return MPC_ERR_HIP;
+  // the layout of mpc_stream_create_cu_reserved: logical CU b is CU b / 8 of
+  // XCD b % 8, so CU j of every XCD goes to part j % parts
+  if (ncu != 256 || strncmp(prop.gcnArchName, "gfx950", 6) != 0) return MPC_ERR_UNSUPPORTED;
+  uint32_t mask[8] = {};
+  for (int b = 0; b < ncu; ++b)
+    if ((b / 8) % parts == part) mask[b / 32] |= 1u << (b % 32);
+  hipStream_t st = nullptr;
+  if (hipExtStreamCreateWithCUMask(&st, 8u, mask) != hipSuccess) return MPC_ERR_HIP;
   *stream = reinterpret_cast<mpc_stream_t>(st);
   return MPC_OK;
 }

@@ -236,6 +236,57 @@ def reference_episode_config(start=(0.0, 0.0, 0.0, 0.0, 0.0), target=(2, 3), see
         max_steps=max_steps, incumbent0=incumbent0, enumerate=int(bool(enumerate)), seed=seed)
 
 
+def logged_step_problems(log, cfg):
+    """The problem and incumbent every logged step of a device episode was
+    solved on, rebuilt on the host from the log records before it — the
+    bookkeeping of episode_advance (csrc/mpc_episode.h) / Episode._advance:
+    t += delta_t per step (math_model_tree.py:302), the pose of the previous
+    record, the incumbent (the episode's first from cfg.incumbent0 or the
+    criterion of the line origin, :676; then float(sys.maxsize), :428), the
+    operator events at cfg.p_turn_right / p_turn_left / p_new_target
+    (:564-569: new target, line origin at the pose) and a restart after a step
+    that ended the episode (ARRIVED / LIMIT / BREAK).  `log`: the records of
+    an episode from its first step on (a fresh DeviceEpisode).  Returns
+    [(mpc_problem_t, incumbent)], one per record."""
+    ended = MPC_EP_ARRIVED | MPC_EP_LIMIT | MPC_EP_BREAK
+
+    def start():
+        return (cfg.start_x, cfg.start_y, cfg.start_phi, 0.0, cfg.target_x, cfg.target_y,
+                cfg.start_x, cfg.start_y)
+
+    def criterion0(xt, yt, x0, y0):
+        if cfg.incumbent0 != 0.0:
+            return cfg.incumbent0
+        saved = (mmt.x_t, mmt.y_t, mmt.x_0, mmt.y_0)
+        mmt.x_t, mmt.y_t, mmt.x_0, mmt.y_0 = xt, yt, x0, y0
+        try:
+            return mmt.control_criterion([x0, y0, 0.0])
+        finally:
+            mmt.x_t, mmt.y_t, mmt.x_0, mmt.y_0 = saved
+
+    x, y, phi, t, xt, yt, x0, y0 = start()
+    inc = criterion0(xt, yt, x0, y0)
+    out = []
+    for rec in log:
+        t = t + cfg.delta_t
+        out.append((make_problem(x, y, phi, xt, yt, x0, y0, cfg.L, t, t + cfg.delta_t), inc))
+        inc = float(sys.maxsize)
+        x, y, phi = rec.x, rec.y, rec.phi
+        if rec.status & ended:
+            x, y, phi, t, xt, yt, x0, y0 = start()
+            inc = criterion0(xt, yt, x0, y0)
+            continue
+        if rec.p == cfg.p_turn_right:
+            xt, yt = mmt._turn_target(x, y, phi, cfg.turn_distance, -1)
+            x0, y0 = x, y
+        if rec.p == cfg.p_turn_left:
+            xt, yt = mmt._turn_target(x, y, phi, cfg.turn_distance, +1)
+            x0, y0 = x, y
+        if rec.p == cfg.p_new_target:
+            xt, yt, x0, y0 = cfg.event_target_x, cfg.event_target_y, x, y
+    return out
+
+
 class DeviceEpisode:
     """The same episode with its state in HBM (mpc_episode_* C ABI): a step
     is enqueued without any host synchronisation, so the host only launches
@@ -416,8 +467,14 @@ class DeviceEpisode:
         return int(t.item())
 
     def close(self):
-        """Release the P2P mailbox and the peers' mappings (idempotent)."""
+        """Release the P2P mailbox and the peers' mappings, and let the
+        overlapped form's side stream drain (idempotent).  Call it before the
+        process group is destroyed: no collective or peer store of this
+        episode may still be in flight when the process exits."""
         L = self.lib
+        if self._comm is not None:
+            self._comm.synchronize()
+            torch.cuda.current_stream().synchronize()
         for p in self._opened:
             L.mpc_ipc_close(ctypes.c_void_p(p))
         self._opened = []
@@ -565,11 +622,23 @@ class DeviceEpisode:
                 "mpc_episode_exchange_flush")
         self.steps_enqueued += 1
 
-    def chain_error(self):
+    def chain_error(self, local=False):
+        """EpisodeState::chain_error — with world > 1 the MAX over the ranks (a
+        collective: every rank calls it), since a rank whose wait timed out
+        posted nothing, so its peers' steps diverge from the true arg-min
+        while their own code stays 0.  local=True: this rank's code only."""
         e = ctypes.c_int32(0)
         native.check(self.lib.mpc_episode_chain_error(self.state.data_ptr(), ctypes.byref(e),
                                                       self._stream()), "mpc_episode_chain_error")
-        return int(e.value)
+        err = int(e.value)
+        if self.world > 1 and not local:
+            import torch.distributed as dist
+            on_dev = dist.get_backend(self.group) == "nccl"
+            t = torch.tensor([err], dtype=torch.int32,
+                             device=self.state.device if on_dev else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            err = int(t.item())
+        return err
 
     def expand(self, events=None, controls=None):
         """Grid + sampler + rollout + finalize for this rank's shard.
@@ -667,9 +736,10 @@ class DeviceEpisode:
     def read_log(self):
         """Complete any pending step, sync, and decode the per-step records.
         Raises ChainError if a chained / exchange step's bounded device wait
-        timed out (mpc_episode_chain_error != 0): such a step ran on
-        speculated constants or dropped this rank's candidate, so its log
-        records must not be trusted."""
+        timed out on ANY rank (chain_error(), reduced over the ranks): such a
+        step ran on speculated constants or dropped a rank's candidate, so
+        the log records must not be trusted.  With world > 1 every rank must
+        call it (the reduction is a collective)."""
         self.flush()
         torch.cuda.current_stream().synchronize()
         err = self.chain_error()
@@ -797,7 +867,9 @@ def cu_reserved_stream(device, reserved_per_xcd=1):
     `reserved_per_xcd` CUs of every XCD free (mpc_stream_create_cu_reserved):
     the launch stream of the overlapped exchange (DeviceEpisode(overlap=True)),
     so that the collective running beside a chained launch always finds CUs.
-    Lives as long as the process."""
+    Lives until the process exits: an atexit hook synchronises the device and
+    destroys it (before the HIP runtime's own teardown, which otherwise finds
+    a stream it did not create still registered)."""
     lib = native.lib()
     p = ctypes.c_void_p()
     with torch.cuda.device(device):
@@ -805,7 +877,48 @@ def cu_reserved_stream(device, reserved_per_xcd=1):
                      "mpc_stream_create_cu_reserved")
     if reserved_per_xcd > 0:
         _CU_RESERVED.add(p.value)
+    if not _CREATED:
+        import atexit
+        atexit.register(_destroy_streams)
+    _CREATED.append((p.value, torch.device(device)))
     return torch.cuda.ExternalStream(p.value, device=device)
+
+
+def cu_share_stream(device, part, parts):
+    """A torch stream on the part-th of `parts` disjoint CU sets of the device
+    (mpc_stream_create_cu_share): the launch stream of each of several ranks
+    that rehearse a multi-GPU run on ONE GPU.  A chained exchange launch
+    larger than one resident round fills every CU with tile blocks waiting for
+    block 0, which waits for the peers — whose launches then find no CU.  On
+    disjoint sets every rank keeps CUs for its block 0.  Destroyed at exit."""
+    lib = native.lib()
+    p = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        native.check(lib.mpc_stream_create_cu_share(int(part), int(parts), ctypes.byref(p)),
+                     "mpc_stream_create_cu_share")
+    if not _CREATED:
+        import atexit
+        atexit.register(_destroy_streams)
+    _CREATED.append((p.value, torch.device(device)))
+    return torch.cuda.ExternalStream(p.value, device=device)
+
+
+_CREATED = []   # (handle, device) of every stream these helpers made
+
+
+def _destroy_streams():
+    """atexit: drain and destroy the streams cu_reserved_stream() made."""
+    lib = native.lib()
+    while _CREATED:
+        h, dev = _CREATED.pop()
+        try:
+            with torch.cuda.device(dev):
+                torch.cuda.synchronize()
+                torch.cuda.set_stream(torch.cuda.default_stream(dev))
+            lib.mpc_stream_destroy(ctypes.c_void_p(h))
+        except Exception:   # the runtime is already gone: nothing left to release
+            pass
+        _CU_RESERVED.discard(h)
 
 
 def tree_episode_config(start, max_calls=None):

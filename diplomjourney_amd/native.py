@@ -40,7 +40,7 @@ EXPORTS = (
     "mpc_fulltree_batched_workspace_bytes", "mpc_fulltree_argmin_batched",
     "mpc_episodes_state_bytes", "mpc_episodes_reset", "mpc_episodes_run",
     "mpc_episode_exchange_step2", "mpc_episode_exchange_mark",
-    "mpc_stream_create_cu_reserved", "mpc_stream_destroy",
+    "mpc_stream_create_cu_reserved", "mpc_stream_create_cu_share", "mpc_stream_destroy",
     "mpc_mailbox_bytes", "mpc_mailbox_alloc", "mpc_mailbox_free", "mpc_mailbox_set_peers",
     "mpc_mailbox_ping",
     "mpc_ipc_handle",
@@ -190,6 +190,8 @@ def lib():
         L.mpc_episode_exchange_mark.argtypes = [_P, ctypes.c_uint32, _P]
         L.mpc_stream_create_cu_reserved.restype = ctypes.c_int
         L.mpc_stream_create_cu_reserved.argtypes = [_I32, ctypes.POINTER(_P)]
+        L.mpc_stream_create_cu_share.restype = ctypes.c_int
+        L.mpc_stream_create_cu_share.argtypes = [_I32, _I32, ctypes.POINTER(_P)]
         L.mpc_stream_destroy.restype = ctypes.c_int
         L.mpc_stream_destroy.argtypes = [_P]
     L.mpc_episode_exchange_flush.restype = ctypes.c_int

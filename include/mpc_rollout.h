@@ -369,8 +369,17 @@ int mpc_episode_exchange_mark(void* state, uint32_t tag, mpc_stream_t stream);
  * overlapped exchange steps on it, so the collective's kernel (RCCL's needs
  * ~280 registers per wave, which never fit beside a chained launch that
  * fills a CU) always finds CUs.  The mask is a property of the stream a
- * kernel or a replayed hipGraph is launched on. */
+ * kernel or a replayed hipGraph is launched on.  MPC_ERR_UNSUPPORTED on any
+ * device but a 256-CU gfx950 (the CU -> XCD layout the mask assumes was
+ * measured there).  Release with mpc_stream_destroy after synchronising. */
 int mpc_stream_create_cu_reserved(int32_t reserved_per_xcd, mpc_stream_t* stream);
+/* A stream whose kernels run on the `part`-th of `parts` disjoint CU sets
+ * (CU j of every XCD belongs to part j % parts): ranks that REHEARSE a
+ * multi-GPU run on fewer GPUs launch on disjoint sets, so one rank's chained
+ * launch (whose tiles wait for block 0, which waits for the peers) can never
+ * occupy the CUs a peer's block 0 needs.  Same device restriction and
+ * release as above. */
+int mpc_stream_create_cu_share(int32_t part, int32_t parts, mpc_stream_t* stream);
 int mpc_stream_destroy(mpc_stream_t stream);
 int mpc_episode_exchange_flush(const mpc_episode_config_t* cfg, void* state, int32_t integrator,
                                const mpc_candidate_t* gathered, int32_t n_gathered,
@@ -469,7 +478,15 @@ int mpc_episode_generate_step(const mpc_episode_config_t* cfg, void* state, int6
  * 2 = cfg's wheelbase form disagreed with the state's; 3 = an exchange step's
  * collection of its block records timed out (`local` then holds none); 4 = an
  * overlapped exchange step's wait for the gathered candidates' mark timed out
- * (the step was not completed: the episode kept its pose).
+ * (the step was not completed: the episode kept its pose); 5 = a P2P exchange
+ * step's wait for the ranks' candidates in its mailbox timed out (a peer did
+ * not run the same step; the step was not completed, and the later steps of
+ * the episode fail fast instead of waiting again).
+ * The waits are bounded on the GPU's wall clock: 0.2 s for a one-GPU chained
+ * launch's tiles; 2 s for block 0's wait for peers or a collective (4, 5); 3 s
+ * for the tiles of an exchange / P2P launch, so a late peer is never scored as
+ * error 1.  A multi-rank caller reduces the code over its ranks (a rank that
+ * timed out posts no candidate, so its peers' steps are suspect too).
  * Reads the device state (syncs). */
 int mpc_episode_chain_error(const void* state, int32_t* error, mpc_stream_t stream);
 

@@ -40,6 +40,27 @@ def _same_choice(got, ref, costs=None):
     return False
 
 
+def _threads():
+    import os
+    try:
+        return max(1, min(16, len(os.sched_getaffinity(0))))
+    except AttributeError:
+        return 8
+
+
+def _report(name, **kv):
+    """Append a parity record to $MPC_PARITY_REPORT (JSON lines), if set, and
+    print it (pytest -s / the captured log)."""
+    import json
+    import os
+    rec = dict(test=name, **kv)
+    print("PARITY", json.dumps(rec))
+    path = os.environ.get("MPC_PARITY_REPORT")
+    if path:
+        with open(path, "a") as fh:
+            fh.write(json.dumps(rec) + "\n")
+
+
 def _close_traj(got, ref, n_steps, tol=STATE_TOL):
     d = max(abs(got.traj[s][k] - ref.traj[s][k]) for s in range(n_steps) for k in range(3))
     assert d <= tol, d
@@ -208,10 +229,16 @@ def test_chained_config_c_events_and_restart_vs_oracle(engine, oracle):
     inside.  Every step's problem is rebuilt on the host with the drop-in's
     own event helpers (_turn_target, new target + line origin at the pose,
     t += dt, reset on a restart, the first incumbent of each episode from its
-    line origin) from the previous log record, and the logged winner is the
-    oracle's full scan of the same batch (8 host threads): same index and
-    (v, beta), the returned pose one of the winner's layer states within 1e-9
-    (finishing logic), or an index disagreement only below 1e-13 relative."""
+    line origin) from the previous log record — and must equal
+    episode.logged_step_problems (the bench's parity leg) — and each batch is
+    scanned in full by the oracle twice:
+      * qk21, the reference's own arithmetic (scipy quad, math_model_tree.py
+        :91-96): the logged winner IS its winner on every step (identity, no
+        tolerance; SURVEY §7 hard part 2) and the costs agree within 1e-12;
+      * rect, the kernel's integrator restated: same index and (v, beta), the
+        returned pose one of the winner's layer states within 1e-9
+        (finishing logic), or an index disagreement only below 1e-13 relative
+        — every use of that branch is counted and reported (MPC_PARITY_REPORT)."""
     from concurrent.futures import ThreadPoolExecutor
     from diplomjourney_amd import math_model_tree as mmt
     from diplomjourney_amd.abi import (MPC_EP_ARRIVED, MPC_EP_BREAK, MPC_EP_EVENT, MPC_EP_LIMIT,
@@ -258,10 +285,24 @@ def test_chained_config_c_events_and_restart_vs_oracle(engine, oracle):
     events = sorted(r.p for r in log if r.status & MPC_EP_EVENT)
     assert events[:3] == [60, 90, 110], events
     assert len({r.episode for r in log}) >= 2                  # a restart inside
-    with ThreadPoolExecutor(max_workers=8) as ex:
+    from diplomjourney_amd.episode import logged_step_problems
+    helper = logged_step_problems(log, ep.cfg)
+    for (pa, ia), (pb, ib) in zip(probs, helper):
+        assert [getattr(pa, f) for f, _ in pa._fields_] == \
+            [getattr(pb, f) for f, _ in pb._fields_] and ia == ib
+    with ThreadPoolExecutor(max_workers=_threads()) as ex:
         futs = [ex.submit(oracle.rollout_argmin, probs[i][0], *host[i % nb], incumbent=probs[i][1],
                           integ="rect", want_costs=True) for i in range(steps)]
+        futq = [ex.submit(oracle.rollout_argmin, probs[i][0], *host[i % nb], incumbent=probs[i][1],
+                          integ="qk21") for i in range(steps)]
         refs = [f.result() for f in futs]
+        refq = [f.result()[0] for f in futq]
+    near_ties, q_noise = [], 0.0
+    for i, (rec, q) in enumerate(zip(log, refq)):     # the reference's arithmetic
+        assert q.found == 1 and rec.index == q.index, (i, rec.index, q.index)
+        assert (rec.v, rec.beta) == (q.v, q.beta), i
+        q_noise = max(q_noise, abs(rec.cost - q.cost) / abs(q.cost))
+    assert q_noise < COST_RTOL, q_noise
     for i, (rec, (ref, costs, _)) in enumerate(zip(log, refs)):
         assert rec.found == ref.found == 1, i
         if rec.index == ref.index:
@@ -273,6 +314,10 @@ def test_chained_config_c_events_and_restart_vs_oracle(engine, oracle):
         else:   # only a near-tie below the ulp noise of the two recurrences
             gap = abs(costs[rec.index] - costs[ref.index]) / abs(costs[ref.index])
             assert gap < 1e-13, (i, rec.index, ref.index, gap)
+            near_ties.append((i, gap))
+    _report("chained_config_c_events_and_restart", steps=steps, candidates=n, horizon=ns,
+            identity_vs_qk21=steps, max_rel_cost_diff_vs_qk21=q_noise,
+            near_tie_branch_vs_rect=len(near_ties), near_ties=near_ties)
 
 
 @pytest.mark.parametrize("integ", ["qk21", "rect+cum"])
@@ -347,15 +392,17 @@ def test_config_d_full_size_sharded_vs_oracle(engine, oracle):
     bench's arithmetic (rect+cum), then the device all-reduce(min+index)
     selection over the 8 records — against the oracle's scan of every shard
     (reference arithmetic, glibc trig, 8 host threads) and its lexicographic
-    minimum: same global index and control, states within 1e-9."""
+    minimum: same global index and control, states within 1e-9 — and the
+    same global index as the oracle's scan in qk21, the reference's own
+    arithmetic (identity, no tolerance; SURVEY §7 hard part 2)."""
     from concurrent.futures import ThreadPoolExecutor
     from diplomjourney_amd.abi import RESULT_BYTES, make_problem
     from diplomjourney_amd.distributed import shard_range
     n, ns, world = 10_000_000, 12, 8
     prob = make_problem(-0.3, 0.4, 2.0, 2, 3, 0, 0, 0.5, 1.0, 1.05)
     gathered = torch.empty(world * RESULT_BYTES, dtype=torch.uint8, device="cuda")
-    futs = []
-    with ThreadPoolExecutor(max_workers=8) as pool:
+    futs, futq = [], []
+    with ThreadPoolExecutor(max_workers=_threads()) as pool:
         for r in range(world):
             lo, hi = shard_range(n, r, world)
             _, _, vs, bs = _sampled(engine, hi - lo, ns, seed=13, base=lo)
@@ -366,12 +413,21 @@ def test_config_d_full_size_sharded_vs_oracle(engine, oracle):
             del vs, bs
             futs.append(pool.submit(oracle.rollout_argmin, prob, vh, bh, index_base=lo,
                                     incumbent=INC_MAX, integ="rect", want_costs=True))
+            futq.append(pool.submit(oracle.rollout_argmin, prob, vh, bh, index_base=lo,
+                                    incumbent=INC_MAX, integ="qk21"))
         refs = [f.result() for f in futs]
+        refq = [f.result()[0] for f in futq]
     out = torch.empty(RESULT_BYTES, dtype=torch.uint8, device="cuda")
     engine.select_winner(gathered, incumbent=INC_MAX, out=out)
     got = engine.fetch(out)
+    q = min(refq, key=lambda x: (x.cost, x.index))
+    assert got.index == q.index and (got.v, got.beta) == (q.v, q.beta), (got.index, q.index)
+    assert math.isclose(got.cost, q.cost, rel_tol=COST_RTOL)
     best = min(range(world), key=lambda r: (refs[r][0].cost, refs[r][0].index))
     ref = refs[best][0]
+    _report("config_d_full_size_sharded", candidates=n, horizon=ns, shards=world,
+            identity_vs_qk21=1, rel_cost_diff_vs_qk21=abs(got.cost - q.cost) / abs(q.cost),
+            near_tie_branch_vs_rect=int(got.index != ref.index))
     if got.index != ref.index:           # only a near-tie below the ulp noise
         lo_g = shard_range(n, 0, world)[1]
         costs = {r: refs[r][1] for r in range(world)}
@@ -396,7 +452,7 @@ def test_exchange_chain_two_ranks_on_one_gpu(engine, tmp_path):
     _run_two_ranks(engine, tmp_path, "gather")
 
 
-def _run_two_ranks(engine, tmp_path, mode):
+def _run_two_ranks(engine, tmp_path, mode, delay_s=0.0):
     import json
     import os
     import socket
@@ -409,14 +465,27 @@ def _run_two_ranks(engine, tmp_path, mode):
         port = s.getsockname()[1]
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    logs = [open(tmp_path / f"rank{r}.log", "wb") for r in range(world)]
     procs = [subprocess.Popen([sys.executable, os.path.join(repo, "tests", "dist_rank.py"),
                                str(r), str(world), str(port), str(n_total), str(ns), str(steps),
-                               str(tmp_path / f"rank{r}.json"), mode], env=env,
-                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                               str(tmp_path / f"rank{r}.json"), mode, str(delay_s)], env=env,
+                              stdout=logs[r], stderr=subprocess.STDOUT)
              for r in range(world)]
-    outs = [p.communicate(timeout=240)[0] for p in procs]
-    for p, o in zip(procs, outs):
-        assert p.returncode == 0, o.decode()[-3000:]
+    import time
+    t_end = time.time() + 150
+    while time.time() < t_end and any(p.poll() is None for p in procs):
+        time.sleep(0.2)
+    hung = [r for r, p in enumerate(procs) if p.poll() is None]
+    for p in procs:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+    for fh in logs:
+        fh.close()
+    outs = [open(tmp_path / f"rank{r}.log", "rb").read() for r in range(world)]
+    for r, (p, o) in enumerate(zip(procs, outs)):
+        assert not hung and p.returncode == 0, (f"rank {r} rc {p.returncode} hung {hung}:\n"
+                                               + o.decode(errors="replace")[-3000:])
     ranks = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
@@ -433,6 +502,7 @@ def _run_two_ranks(engine, tmp_path, mode):
         assert rk["chain_error"] == 0
         assert rk["log"] == want
     assert ranks[0]["winner"] == ranks[1]["winner"] == one.local.cpu().tolist()
+    return ranks
 
 
 def test_c_host_exchange_episode(engine, tmp_path):
@@ -1051,6 +1121,17 @@ def test_p2p_exchange_two_ranks_on_one_gpu(engine, tmp_path):
     _run_two_ranks(engine, tmp_path, "p2p")
 
 
+def test_p2p_exchange_with_a_lagging_rank(engine, tmp_path):
+    """A rank that runs late (ranks are not barrier-aligned between
+    steps): rank 1 holds its stream back ~0.3 s (a spinning kernel) before
+    its 10th step, so rank 0's launches wait in block 0 for its candidate while
+    their tile blocks wait for block 0.  The tiles' bound (3 s) outlasts block
+    0's peer wait (2 s), so the lag is absorbed: both ranks log exactly the
+    single-rank episode, chain_error 0 on both."""
+    ranks = _run_two_ranks(engine, tmp_path, "p2p", delay_s=0.3)
+    assert ranks[1]["held_ms"] > 200, ranks[1]["held_ms"]
+
+
 def test_overlapped_exchange_with_a_late_collective(engine):
     """The overlapped exchange step (mpc_episode_exchange_step2): the
     all_gather of step k runs on a side stream beside launch k+1, whose block
@@ -1114,7 +1195,7 @@ def test_bench_contract(extra):
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--steps", "8",
                         "--warmup", "2", "--cpu-seconds", "0", "--no-second-pass"] + extra,
-                       capture_output=True, text=True, timeout=110, cwd=repo)
+                       capture_output=True, text=True, timeout=200, cwd=repo)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -1142,6 +1223,12 @@ def test_bench_contract(extra):
         assert d["config"]["step_launches"].startswith("chained")
         ro = d["roofline_rollout_only"]
         assert ro["kernel"] == "k_rollout_argmin_stream" and 0 < ro["frac"] < 1
+        # the reference arithmetic's winner on every parity step (oracle qk21)
+        assert d["parity"]["identity_rate"] == 1.0 and d["parity"]["steps"] == 8, d["parity"]
+        cd = d["config_d"]      # BASELINE config D's one-GPU share in the same run
+        assert cd["chain_error"] == 0 and cd["config"]["candidates_per_gpu"] == 1_250_000
+        assert cd["roofline"]["kernel"] == "k_episode_chain"
+        assert cd["roofline"]["algorithmic_bytes_per_launch"] == 16.0 * 12 * 1_250_000
     assert rf["traffic"] is not None and abs(rf["traffic"] / 160e6 - 1) < 0.01
 
 
@@ -1157,11 +1244,13 @@ def test_bench_two_ranks_spawned(mode):
     import subprocess
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    # the driver's own form (--steps 20 --warmup 5, second input pass, parity
+    # check and config-D sub-result included); gloo and a smaller config-C
+    # shard only because both ranks share this one GPU
     r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2",
-                        "--dist-backend", "gloo", "--candidates-per-gpu", "100000", "--steps", "8",
-                        "--warmup", "2", "--cpu-seconds", "0", "--no-second-pass",
-                        "--exchange-mode", mode],
-                       capture_output=True, text=True, timeout=110, cwd=repo, env=env)
+                        "--dist-backend", "gloo", "--candidates-per-gpu", "100000", "--steps", "20",
+                        "--warmup", "5", "--exchange-mode", mode],
+                       capture_output=True, text=True, timeout=300, cwd=repo, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -1174,9 +1263,19 @@ def test_bench_two_ranks_spawned(mode):
     else:
         assert "all_gather(536 B candidates)" in d["config"]["parallelism"]
     rf = d["roofline"]
-    assert rf["kernel"] == ("k_episode_chain[p2p]" if mode == "p2p"
-                            else "k_episode_chain[exchange]") and 0 < rf["frac"] < 1
+    kern = "k_episode_chain[p2p]" if mode == "p2p" else "k_episode_chain[exchange]"
+    assert rf["kernel"] == kern and 0 < rf["frac"] < 1
     assert rf["algorithmic_bytes_per_launch"] == 16.0 * 10 * 100_000
+    # the sampled second pass (expand + advance: the 808-B all_gather) ran
+    assert d["other_inputs"]["inputs"] == "sampled" and d["other_inputs"]["value"] > 0
+    # every parity step's winner is the reference arithmetic's (oracle qk21)
+    assert d["parity"]["identity_rate"] == 1.0, d["parity"]
+    # BASELINE config D in the same run: N=12, 1.25e6 per GPU, same step form
+    cd = d["config_d"]
+    assert cd["chain_error"] == 0 and cd["value"] > 0
+    assert cd["config"]["n_steps"] == 12 and cd["config"]["candidates_total"] == 2_500_000
+    assert cd["roofline"]["kernel"] == kern
+    assert cd["roofline"]["algorithmic_bytes_per_launch"] == 16.0 * 12 * 1_250_000
 
 
 def test_bench_workload_a_parity():

@@ -79,10 +79,11 @@ def build():
         ("  records_candidate(part_prev, n_part_prev, v_prev, b_prev, n_cand, n_steps, index_base, lc);\n",
          "  records_candidate(part_prev, n_part_prev, v_prev, b_prev, n_cand, n_steps, index_base, lc);\n"
          f"  {b0(1)}\n"),
-        ("  post_candidate(s_peers, s_rank, world, prev, n_steps, lc);\n",
-         f"  post_candidate(s_peers, s_rank, world, prev, n_steps, lc);\n  {b0(2)}\n"),
-        ("  const mpc_candidate_t* g = wait_mailbox(S, mb, prev, world, n_steps);\n",
-         f"  const mpc_candidate_t* g = wait_mailbox(S, mb, prev, world, n_steps);\n  {b0(3)}\n"),
+        ("  post_candidate(s_peers, s_rank, world, prev, slot, n_steps, lc);\n",
+         f"  post_candidate(s_peers, s_rank, world, prev, slot, n_steps, lc);\n  {b0(2)}\n"),
+        ("      wait_mailbox(S, mb, prev, slot, world, n_steps, s_err ? 0ull : kPeerWaitTicks);\n",
+         "      wait_mailbox(S, mb, prev, slot, world, n_steps, s_err ? 0ull : kPeerWaitTicks);\n"
+         f"  {b0(3)}\n"),
         ("               kPubWords, publish_epoch);\n  emit_winner_tail",
          f"               kPubWords, publish_epoch);\n  {b0(8)}\n  emit_winner_tail"),
         ("  EpisodeHead* S = &H;\n  S->steps_for_slowing -= 1;\n",
