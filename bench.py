@@ -1074,7 +1074,11 @@ def traffic_summary(traffic_json, kernel, bytes_launch):
 VALU_JSON = {("k_episode_chain", "rect+cum"): ("r04_final/valu/chain.json", 1_000_000, 10),
              ("k_rollout_argmin_stream", "qk21"): ("r04_final/valu/qk21.json", 1_000_000, 10),
              ("k_rollout_generated", "rect+cum"): ("r04_final/valu/gen.json", 1_000_000, 10),
-             ("k_ft_leaves", "rect+rot"): ("r04_final/valu/ft.json", 451 ** 3, 3)}
+             ("k_ft_leaves", "rect+rot"): ("r04_final/valu/ft.json", 451 ** 3, 3),
+             # the device-resident episode drivers: the whole run is ONE launch;
+             # keyed (episodes, max_calls) of workloads R and G as the bench runs them
+             ("k_episodes_run", "qk21"): ("r05/valu/episodes_R.json", 1000, 1000),
+             ("k_ft_episodes_run", "rect+rot"): ("r05/valu/ftepisodes_G.json", 1000, 50)}
 
 
 def valu_roofline(kernel, integrator, ms, n_cand, n_steps, note=None):
@@ -1395,7 +1399,14 @@ def bench_tree_episodes(args, wl, eng, rank, world, cpu):
         "episodes_per_s": wl["robots"] / elapsed,
         "p50_ms": None,
         "p50_note": "ms_per_step = the run's time / the longest episode's MPC calls",
-        "roofline": None, "cpu_baseline": cpu,
+        "roofline": None,
+        "roofline_valu": valu_roofline("k_episodes_run", args.integrator, elapsed * 1e3,
+                                       wl["robots"], args.steps,
+                                       note="counted fp64 ops of the whole one-launch run "
+                                            "(PMC, tools/prof_kernel.py tree_episodes) over the "
+                                            "timed run; the candidates never touch HBM, so "
+                                            "the fp64 VALU is the bound"),
+        "cpu_baseline": cpu,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -1405,9 +1416,11 @@ def bench_tree_episodes(args, wl, eng, rank, world, cpu):
 
 def bench_episodes(args, wl, eng, rank, world, cpu):
     """Config G: the script's episode loop for 1000 episodes at once (robots
-    sharded over ranks, no exchange).  A timed step = one batched full-tree
-    launch over every still-running robot + the host episode updates; K steps
-    of run_batched (episodes stopped by --steps as max_calls)."""
+    sharded over ranks, no exchange), device-resident (run_batched ->
+    mpc_fulltree_episodes_run: one block per robot runs its episode's
+    full-tree calls back to back in ONE launch).  Timed: up to K = --steps
+    calls of every episode (K as max_calls) between syncs; ms_per_step = that
+    time / the longest episode's calls (a lockstep-equivalent step)."""
     import math as _m
     import torch
     import torch.distributed as dist
@@ -1418,37 +1431,57 @@ def bench_episodes(args, wl, eng, rank, world, cpu):
     s1 = int(rmm.size_max_1)
     starts = rmm.draw_starts(wl["robots"], seed=20261015)
     lo, hi = shard_range(len(starts), rank, world)
-    rmm.run_batched(starts[lo:hi], max_calls=max(1, args.warmup))      # warmup
+    for _ in range(max(1, args.warmup // 20)):                           # warmup: whole runs
+        rmm.run_batched(starts[lo:hi], max_calls=args.steps)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    stats = {}
     t0 = time.perf_counter()
-    outs = rmm.run_batched(starts[lo:hi], max_calls=args.steps)
+    outs = rmm.run_batched(starts[lo:hi], max_calls=args.steps, stats=stats)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     robot_steps = sum(len(r) for r, _ in outs)
-    t = torch.tensor([elapsed, robot_steps], dtype=torch.float64, device=eng.device)
+    t = torch.tensor([elapsed, robot_steps, stats["steps"]], dtype=torch.float64,
+                     device=eng.device)
     if world > 1:
-        mx = t[:1].clone()
+        mx = t[[0, 2]].clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        elapsed, robot_steps = float(mx.item()), float(t[1].item())
+        t[0], t[2] = mx[0], mx[1]
+    elapsed, robot_steps, lockstep = float(t[0]), float(t[1]), int(t[2])
     leaves = robot_steps * s1 ** 3
     stops = {}
     for _, st in outs:
         stops[st] = stops.get(st, 0) + 1
+    flops = FT_FLOPS_PER_LEAF[args.integrator] * leaves / world / elapsed      # per GPU
     out = {
         "metric": METRIC, "value": leaves / elapsed, "unit": "leaves/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / max(1, lockstep) * 1e3,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic",
+        "data": "synthetic (the script's seeded start/target draws)",
         "config": {"workload": wl["desc"], "s1": s1, "robots": wl["robots"],
-                   "robot_steps": robot_steps, "integrator": args.integrator,
-                   "episode_stops_rank0": stops,
+                   "robot_steps": robot_steps, "lockstep_steps": lockstep,
+                   "integrator": args.integrator, "episode_stops_rank0": stops,
+                   "episode_loop": "device-resident: one block per robot, one launch for all "
+                                   "calls (mpc_fulltree_episodes_run)",
                    "parallelism": f"robot-sharded x{world}, no exchange"},
-        "roofline": None, "cpu_baseline": cpu,
+        "p50_note": "ms_per_step = the run's time (host, incl. the log read-back) / the "
+                    "longest episode's calls",
+        "roofline": {"bound": "valu-fp64", "achieved": flops / 1e12,
+                     "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": flops / 1e12 / FP64_VECTOR_PEAK_TFLOPS, "traffic": None,
+                     "kernel": "k_ft_episodes_run",
+                     "note": "algorithmic fp64 ops per leaf as written (FT_FLOPS_PER_LEAF) x "
+                             "the leaves scored, over the whole timed run"},
+        "roofline_valu": valu_roofline("k_ft_episodes_run", args.integrator, elapsed * 1e3,
+                                       wl["robots"], args.steps,
+                                       note="counted fp64 ops of the whole run (PMC) over the "
+                                            "timed run"),
+        "cpu_baseline": cpu,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -85,6 +85,14 @@ class MpcEpisodeConfig(ctypes.Structure):
 # mpc_episode_log_t.status bits (include/mpc_rollout.h)
 MPC_EP_STALE, MPC_EP_STUCK, MPC_EP_BREAK, MPC_EP_EVENT, MPC_EP_ARRIVED, MPC_EP_LIMIT = (
     1, 2, 4, 8, 16, 32)
+MPC_EP_NO_TRAJ = 64     # full-tree episodes: the first call found no winning leaf
+
+
+class MpcFulltreeEpisodeConfig(ctypes.Structure):
+    """mpc_fulltree_episode_config_t: one run_math_model.py episode (:231-280)."""
+    _fields_ = [(n, ctypes.c_double) for n in (
+        "x_0", "y_0", "phi_0", "x_t", "y_t", "atan_target", "incumbent0")] + [
+        ("max_calls", ctypes.c_int32), ("reserved_", ctypes.c_int32)]
 
 
 class MpcEpisodeLog(ctypes.Structure):

@@ -96,15 +96,15 @@ __global__ __launch_bounds__(kBlock) void k_ft_controls(Consts K, const double* 
 constexpr int kFtChunk = 256;  // k2 per wave-item
 constexpr int kFtWaves = 7;    // launch bound (waves per SIMD): <= 72 VGPRs, no scratch (8 spills)
 
+// wave / n_waves: this wave's rank among the waves that share the items (the
+// launch's waves; a block's own in the device-resident episodes)
 template <int INTEG, bool ROT>
 __device__ __forceinline__ void ft_leaves_body(const Consts& K, double atan_t,
                                                const FtCtl* __restrict__ ctl, int64_t s1,
                                                int64_t item_lo, int64_t item_hi,
-                                               uint64_t& best_k, int64_t& best_i) {
+                                               uint64_t& best_k, int64_t& best_i, int64_t wave,
+                                               int64_t n_waves) {
   const int lane = threadIdx.x & 63;
-  const int64_t wave = static_cast<int64_t>(blockIdx.x) * kWaves +
-                       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t n_waves = static_cast<int64_t>(gridDim.x) * kWaves;
   const int64_t n_pairs = s1 * s1;
   const int64_t n_chunks = (s1 + kFtChunk - 1) / kFtChunk;
   double best_c = key_cost(best_k);   // (+inf: none yet)
@@ -154,10 +154,15 @@ __global__ __launch_bounds__(kBlock, kFtWaves) void k_ft_leaves(Consts K, double
                                                       int64_t item_hi, Rec* __restrict__ part) {
   uint64_t best_k = ~0ull;
   int64_t best_i = INT64_MAX;
+  const int64_t wave = static_cast<int64_t>(blockIdx.x) * kWaves +
+                       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t n_waves = static_cast<int64_t>(gridDim.x) * kWaves;
   if (ROT && *no_rot == 0u)
-    ft_leaves_body<INTEG, true>(K, atan_t, ctl, s1, item_lo, item_hi, best_k, best_i);
+    ft_leaves_body<INTEG, true>(K, atan_t, ctl, s1, item_lo, item_hi, best_k, best_i, wave,
+                                n_waves);
   else
-    ft_leaves_body<INTEG, false>(K, atan_t, ctl, s1, item_lo, item_hi, best_k, best_i);
+    ft_leaves_body<INTEG, false>(K, atan_t, ctl, s1, item_lo, item_hi, best_k, best_i, wave,
+                                 n_waves);
   block_argmin(best_k, best_i);
   if (threadIdx.x == 0) part[blockIdx.x] = Rec{best_k, best_i};
 }
@@ -253,10 +258,13 @@ __global__ __launch_bounds__(kBlock, kFtWaves) void k_ft_leaves_batched(
   const int64_t n_items = ((s1 * s1 + 63) / 64) * ((s1 + kFtChunk - 1) / kFtChunk);
   uint64_t best_k = ~0ull;
   int64_t best_i = INT64_MAX;
+  const int64_t wave = static_cast<int64_t>(blockIdx.x) * kWaves +
+                       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t n_waves = static_cast<int64_t>(gridDim.x) * kWaves;
   if (ROT && *no_rot == 0u)
-    ft_leaves_body<INTEG, true>(K, atan_t, ctl, s1, 0, n_items, best_k, best_i);
+    ft_leaves_body<INTEG, true>(K, atan_t, ctl, s1, 0, n_items, best_k, best_i, wave, n_waves);
   else
-    ft_leaves_body<INTEG, false>(K, atan_t, ctl, s1, 0, n_items, best_k, best_i);
+    ft_leaves_body<INTEG, false>(K, atan_t, ctl, s1, 0, n_items, best_k, best_i, wave, n_waves);
   block_argmin(best_k, best_i);
   if (threadIdx.x == 0) part[static_cast<int64_t>(r) * gridDim.x + blockIdx.x] =
       Rec{best_k, best_i};

@@ -18,6 +18,7 @@
 #include "../../include/mpc_rollout.h"
 #include "mpc_comm.h"
 #include "mpc_episode.h"
+#include "mpc_ftepisodes.h"
 #include "mpc_episodes.h"
 #include "mpc_fulltree.h"
 #include "mpc_kernels.h"
@@ -1128,6 +1129,53 @@ int mpc_fulltree_argmin_batched(const mpc_fulltree_problem_t* problems,
         robots, ctl, no_rot, s1, part);
     k_ft_finalize_batched<I, R><<<n_problems, kBlock, 0, st>>>(
         part, static_cast<int>(bx), robots, ctl, no_rot, s1, incumbents, out);
+  });
+  return last_hip_status();
+}
+
+// ----------------------------- full-tree episodes ----------------------------
+size_t mpc_fulltree_episodes_state_bytes(int32_t n_robots) {
+  if (n_robots < 1) return 0;
+  return ft_align(static_cast<size_t>(n_robots) * sizeof(FtEpisode)) +
+         static_cast<size_t>(n_robots) * sizeof(mpc_fulltree_episode_config_t);
+}
+
+int mpc_fulltree_episodes_reset(const mpc_fulltree_episode_config_t* cfgs, int32_t n_robots,
+                                void* state, mpc_stream_t stream) {
+  if (!cfgs || !state || n_robots < 1 || n_robots > 65535) return MPC_ERR_ARG;
+  for (int32_t r = 0; r < n_robots; ++r)
+    if (cfgs[r].max_calls < 0) return MPC_ERR_ARG;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  char* s = static_cast<char*>(state);
+  auto* dcfg = reinterpret_cast<mpc_fulltree_episode_config_t*>(
+      s + ft_align(static_cast<size_t>(n_robots) * sizeof(FtEpisode)));
+  // (pageable host source: the copy has read it when the call returns)
+  if (hipMemcpyAsync(dcfg, cfgs, static_cast<size_t>(n_robots) * sizeof(*cfgs),
+                     hipMemcpyHostToDevice, st) != hipSuccess)
+    return MPC_ERR_HIP;
+  k_ft_episodes_reset<<<static_cast<unsigned>(cdiv(n_robots, 256)), 256, 0, st>>>(
+      dcfg, n_robots, reinterpret_cast<FtEpisode*>(s));
+  return last_hip_status();
+}
+
+int mpc_fulltree_episodes_run(void* state, int32_t n_robots, const double* v_grid, int32_t n_v,
+                              const double* beta_grid, int32_t n_beta, double L, double delta_t,
+                              double eps, int32_t integrator, int32_t max_calls,
+                              mpc_episode_log_t* log, int32_t log_capacity,
+                              mpc_episodes_progress_t* progress, mpc_stream_t stream) {
+  if (!state || !v_grid || !beta_grid || n_robots < 1 || n_robots > 65535 || n_v < 1 ||
+      n_beta < 1 || max_calls < 0 || log_capacity < 0 || (log && log_capacity < 1) ||
+      !(L > 0.0) || !(delta_t > 0.0))
+    return MPC_ERR_ARG;
+  if (static_cast<int64_t>(n_v) * n_beta > kFtEpMaxS1) return MPC_ERR_UNSUPPORTED;
+  if (mode_ok(integrator, false) != MPC_OK) return MPC_ERR_UNSUPPORTED;
+  if (max_calls == 0) return MPC_OK;
+  dispatch_mode2(integrator, [&](auto integ, auto rot) {
+    constexpr int I = decltype(integ)::value;
+    constexpr bool R = decltype(rot)::value;
+    k_ft_episodes_run<I, R><<<n_robots, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        reinterpret_cast<FtEpisode*>(state), v_grid, n_v, beta_grid, n_beta, L, delta_t, eps,
+        max_calls, log, log ? log_capacity : 0, progress);
   });
   return last_hip_status();
 }

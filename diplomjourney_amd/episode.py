@@ -837,6 +837,49 @@ class DeviceEpisodes:
         return out
 
 
+class DeviceFtEpisodes:
+    """R robots' run_math_model.py episodes with the script's own full-tree MPC
+    step, in HBM (mpc_fulltree_episodes_*, csrc/mpc_ftepisodes.h): one block per
+    robot runs its episode's calls back to back, `run(k)` is ONE launch of up
+    to k calls of every robot.  cfgs: MpcFulltreeEpisodeConfig per robot;
+    v_grid / beta_grid: the script's grids as device tensors."""
+
+    def __init__(self, engine, cfgs, v_grid, beta_grid, L, delta_t, eps, integrator="qk21",
+                 log_capacity=256):
+        from .abi import INTEGRATORS, MpcFulltreeEpisodeConfig, PROGRESS_BYTES
+        self.lib = native.lib()
+        self.cfgs = (MpcFulltreeEpisodeConfig * len(cfgs))(*cfgs)
+        self.R = len(cfgs)
+        self.vg, self.bg = v_grid, beta_grid
+        self.L, self.delta_t, self.eps = float(L), float(delta_t), float(eps)
+        self._integ = INTEGRATORS[integrator]
+        dev = engine.device
+        self.state = torch.zeros(self.lib.mpc_fulltree_episodes_state_bytes(self.R),
+                                 dtype=torch.uint8, device=dev)
+        self.log_capacity = int(log_capacity)
+        self.log = torch.zeros(self.R * self.log_capacity * LOG_BYTES, dtype=torch.uint8,
+                               device=dev)
+        self.progress = torch.zeros(self.R * PROGRESS_BYTES, dtype=torch.uint8, device=dev)
+        self.reset()
+
+    def reset(self):
+        native.check(self.lib.mpc_fulltree_episodes_reset(ctypes.byref(self.cfgs), self.R,
+                                                          self.state.data_ptr(), _stream()),
+                     "mpc_fulltree_episodes_reset")
+        self.progress.zero_()
+
+    def run(self, max_calls):
+        """Enqueue up to max_calls MPC calls of every still-running robot."""
+        native.check(self.lib.mpc_fulltree_episodes_run(
+            self.state.data_ptr(), self.R, self.vg.data_ptr(), self.vg.numel(),
+            self.bg.data_ptr(), self.bg.numel(), self.L, self.delta_t, self.eps, self._integ,
+            int(max_calls), self.log.data_ptr(), self.log_capacity, self.progress.data_ptr(),
+            _stream()), "mpc_fulltree_episodes_run")
+
+    read_progress = DeviceEpisodes.read_progress   # (calls, stop, leaves) per robot
+    read_logs = DeviceEpisodes.read_logs
+
+
 def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 

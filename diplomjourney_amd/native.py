@@ -46,6 +46,8 @@ EXPORTS = (
     "mpc_ipc_handle",
     "mpc_ipc_open", "mpc_ipc_close", "mpc_peer_enable", "mpc_episode_p2p_step",
     "mpc_episode_p2p_flush",
+    "mpc_fulltree_episodes_state_bytes", "mpc_fulltree_episodes_reset",
+    "mpc_fulltree_episodes_run",
 )
 
 HIPCC_FLAGS = [
@@ -241,6 +243,15 @@ def lib():
         L.mpc_episodes_reset.argtypes = [_P, _I32, _P, _P]
         L.mpc_episodes_run.restype = ctypes.c_int
         L.mpc_episodes_run.argtypes = [_P, _I32, _I32, _I32, _I32, _P, _I32, _P, _P]
+    if not (_LIB_OVERRIDE and not hasattr(L, "mpc_fulltree_episodes_run")):
+        L.mpc_fulltree_episodes_state_bytes.restype = ctypes.c_size_t
+        L.mpc_fulltree_episodes_state_bytes.argtypes = [_I32]
+        L.mpc_fulltree_episodes_reset.restype = ctypes.c_int
+        L.mpc_fulltree_episodes_reset.argtypes = [_P, _I32, _P, _P]
+        L.mpc_fulltree_episodes_run.restype = ctypes.c_int
+        L.mpc_fulltree_episodes_run.argtypes = [
+            _P, _I32, _P, _I32, _P, _I32, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+            _I32, _I32, _P, _I32, _P, _P]
     _lib = L
     return L
 

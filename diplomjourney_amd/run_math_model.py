@@ -238,13 +238,67 @@ class _Robot:
         return 10000 * dist_t + 10 * angle ** 2 + 100 * 1000 ** 2
 
 
-def run_batched(starts, max_calls=None, integrator=None):
+def run_batched(starts, max_calls=None, integrator=None, chunk=256, stats=None):
+    """The script's episode loop (:231-280) for len(starts) episodes at once,
+    device-resident (mpc_fulltree_episodes_run, csrc/mpc_ftepisodes.h): one
+    robot per episode, one block per robot runs its episode's full-tree MPC
+    steps back to back — the stop rules, t += delta_t, the S1^3 leaves against
+    the robot's never-reset incumbent, its stale winner, the two-non-move stop —
+    `chunk` calls per launch with no host step in between.  Returns
+    [(records, stop)] per episode, as run_episode does (records rebuilt from
+    the per-step log: pre = (x, y, phi, v, t, optimal_criterion) before the
+    call, ret, optimal_criterion after it); raises the script's TypeError if an
+    episode's first call finds no winner.  stats (optional dict) receives the
+    lockstep-equivalent steps (the longest episode's calls) and the leaves."""
+    import numpy as np
+    from .abi import (MPC_EP_ARRIVED, MPC_EP_BREAK, MPC_EP_NO_TRAJ, MpcFulltreeEpisodeConfig)
+    from .episode import DeviceFtEpisodes
+    eng, (vg, bg) = _device()
+    integ = INTEGRATOR if integrator is None else integrator
+    robots = [_Robot(s) for s in starts]
+    cfgs = [MpcFulltreeEpisodeConfig(float(r.x_0), float(r.y_0), float(r.phi_0), float(r.x_t),
+                                     float(r.y_t), r.atan_t, float(r.crit), int(max_calls or 0), 0)
+            for r in robots]
+    cap = min(chunk, max_calls) if max_calls else chunk
+    eps_dev = DeviceFtEpisodes(eng, cfgs, vg, bg, float(L), float(delta_t), float(eps), integ,
+                               log_capacity=cap)
+    logs = [[] for _ in robots]
+    while True:
+        eps_dev.run(cap)
+        for r, lg in enumerate(eps_dev.read_logs(first_step=[len(x) for x in logs])):
+            logs[r].extend(lg)
+        calls, stop, leaves = eps_dev.read_progress()
+        if (stop != 0).all():
+            break
+    if stats is not None:
+        stats["steps"] = stats.get("steps", 0) + int(calls.max(initial=0))
+        stats["leaves"] = stats.get("leaves", 0) + int(leaves.sum())
+    out = []
+    for r, lg, st in zip(robots, logs, stop):
+        if st & MPC_EP_NO_TRAJ:
+            raise TypeError("'int' object is not subscriptable")   # [0][0], as the script
+        recs = []
+        x, y, phi, v, t, crit = r.x, r.y, r.phi, r.v, r.t, r.crit
+        for g in lg:
+            ret = [float(g["x"]), float(g["y"]), float(g["phi"]), float(g["v"]), float(g["beta"])]
+            recs.append({"pre": (x, y, phi, v, t, crit), "ret": ret,
+                         "optimal_criterion": float(g["cost"])})
+            x, y, phi, v = ret[:4]
+            t = t + delta_t
+            crit = float(g["cost"])
+        out.append((recs, "recursive_error" if st & MPC_EP_BREAK else
+                    "on_target" if st & MPC_EP_ARRIVED else "max_calls"))
+    return out
+
+
+def run_batched_lockstep(starts, max_calls=None, integrator=None):
     """The script's episode loop (:231-280) for len(starts) episodes at once:
     one robot per episode, all robots step in lockstep, and every MPC step of
     all still-running episodes is ONE batched full-tree launch
-    (mpc_fulltree_argmin_batched).  Each robot keeps its own never-reset
-    incumbent, stale winner and stop rule.  Returns [(records, stop)] per
-    episode, as run_episode does."""
+    (mpc_fulltree_argmin_batched) with the episode updates on the host (round
+    3's driver, kept as the device-resident run_batched's cross-check).  Each
+    robot keeps its own never-reset incumbent, stale winner and stop rule.
+    Returns [(records, stop)] per episode, as run_episode does."""
     eng, (vg, bg) = _device()
     integ = INTEGRATOR if integrator is None else integrator
     robots = [_Robot(s) for s in starts]
@@ -398,7 +452,8 @@ def run_tree_batched(starts, max_calls=None, integrator="qk21", engine=None, sta
     return [(records[r], names[r]) for r in range(R)]
 
 
-__all__ = ["configure", "shard_over", "draw_starts", "run_batched", "is_on_target",
+__all__ = ["configure", "shard_over", "draw_starts", "run_batched", "run_batched_lockstep",
+           "is_on_target",
            "get_distance_from_line", "get_distance_from_target", "saturation", "control_criterion",
            "predictive_control", "start_episode", "run_episode", "prediction_horizon",
            "run_tree_episode", "run_tree_batched"]

@@ -576,6 +576,46 @@ int mpc_fulltree_argmin_batched(const mpc_fulltree_problem_t* problems,
                                 void* ws, size_t ws_bytes, mpc_fulltree_result_t* out,
                                 mpc_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * Full-tree episodes, device-resident: run_math_model.py's
+ * episode loop (:231-280) with its OWN full-tree MPC step (:133-228, the tree
+ * of mpc_fulltree_argmin) for R robots, one robot per episode.  ONE launch
+ * runs up to max_calls MPC steps of every robot (one block per robot, per-robot
+ * state in HBM, no host round trip, no lockstep): the stop rules before each
+ * call (on target :261, the robot's max_calls), t += delta_t (:156), the S1^3
+ * leaves scored with the heading-term criterion, strict < against the robot's
+ * never-reset optimal_criterion (:193-196), the winner's first layer as the
+ * returned state (or the stale one when no leaf wins), the two-non-move stop
+ * (:266-272).  Repeated launches continue the episodes.
+ *   mpc_fulltree_episodes_reset  copies the R configurations (host array; the
+ *                                caller evaluates the script's expressions for
+ *                                atan_target and incumbent0) into the state
+ *   mpc_fulltree_episodes_run    v_grid / beta_grid: device arrays, S1 <= 512;
+ *                                log: [R][log_capacity] rings (slot = step %
+ *                                capacity; cost = optimal_criterion after the
+ *                                call, index = the winning leaf or -1); progress:
+ *                                {calls, stop, leaves scored} per robot
+ * A robot whose first call finds no winning leaf stops with MPC_EP_NO_TRAJ (the
+ * script raises TypeError there: optimal_trajectory is still [0]).
+ * ------------------------------------------------------------------------- */
+#define MPC_EP_NO_TRAJ 64
+typedef struct mpc_fulltree_episode_config {
+  double x_0, y_0, phi_0;     /* start (:235-237)                                    */
+  double x_t, y_t;            /* target (:238-239)                                   */
+  double atan_target;         /* numpy arctan(x_t / y_t) (:83)                       */
+  double incumbent0;          /* control_criterion([x_0, y_0, phi_0]) (:252)        */
+  int32_t max_calls;          /* MPC calls after which the episode stops; 0 = none  */
+  int32_t reserved_;
+} mpc_fulltree_episode_config_t;
+size_t mpc_fulltree_episodes_state_bytes(int32_t n_robots);
+int mpc_fulltree_episodes_reset(const mpc_fulltree_episode_config_t* cfgs, int32_t n_robots,
+                                void* state, mpc_stream_t stream);
+int mpc_fulltree_episodes_run(void* state, int32_t n_robots, const double* v_grid, int32_t n_v,
+                              const double* beta_grid, int32_t n_beta, double L, double delta_t,
+                              double eps, int32_t integrator, int32_t max_calls,
+                              mpc_episode_log_t* log, int32_t log_capacity,
+                              mpc_episodes_progress_t* progress, mpc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

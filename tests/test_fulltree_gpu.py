@@ -172,6 +172,59 @@ def test_batched_equals_sequential_episodes(engine):
         rmm.configure()
 
 
+@pytest.mark.parametrize("integ", ["qk21", "rect+rot"])
+def test_device_episodes_equal_lockstep_driver(engine, integ):
+    """Workload G's driver, device-resident (run_batched ->
+    mpc_fulltree_episodes_run: one block per robot runs its episode's
+    full-tree calls back to back in one launch) == the host lockstep driver
+    (run_batched_lockstep: one batched full-tree launch per lockstep step, host
+    updates), record for record: the same returned states and controls
+    (bitwise), incumbents and stops, for 48 of the script's episodes at
+    G's grid (S1 = 5 x 13)."""
+    from diplomjourney_amd import run_math_model as rmm
+    rmm.configure(0.25, math.radians(10))
+    try:
+        starts = rmm.draw_starts(48, seed=3)
+        dev = rmm.run_batched(starts, max_calls=9, integrator=integ)
+        ref = rmm.run_batched_lockstep(starts, max_calls=9, integrator=integ)
+        assert sum(len(r) for r, _ in dev) > 100
+        for (rd, sd), (rr, sr) in zip(dev, ref):
+            assert sd == sr and len(rd) == len(rr)
+            for a, b in zip(rd, rr):
+                assert a["ret"] == b["ret"] and a["optimal_criterion"] == b["optimal_criterion"]
+                assert a["pre"] == b["pre"]
+        # chunked launches continue the episodes: 4 calls per launch == one launch
+        assert rmm.run_batched(starts, max_calls=9, integrator=integ, chunk=4) == dev
+    finally:
+        rmm.configure()
+
+
+def test_device_episodes_no_winner_raises_as_the_script(engine, monkeypatch):
+    """A first call with no leaf below the first incumbent leaves the script's
+    optimal_trajectory at [0] and raises TypeError: both drivers do (the
+    first incumbent forced to 0, which no criterion value is below); on the
+    device the robot stops after that call with MPC_EP_NO_TRAJ."""
+    from diplomjourney_amd import run_math_model as rmm
+    from diplomjourney_amd.abi import MPC_EP_NO_TRAJ, MpcFulltreeEpisodeConfig
+    from diplomjourney_amd.episode import DeviceFtEpisodes
+    rmm.configure(0.25, math.radians(10))
+    try:
+        starts = rmm.draw_starts(4, seed=5)
+        monkeypatch.setattr(rmm._Robot, "_criterion0", lambda self: 0.0)
+        for fn in (rmm.run_batched, rmm.run_batched_lockstep):
+            with pytest.raises(TypeError):
+                fn(starts, max_calls=3, integrator="rect+rot")
+        eng, (vg, bg) = rmm._device()
+        cfg = MpcFulltreeEpisodeConfig(*starts[0], float(np.arctan(starts[0][3] / starts[0][4])),
+                                       0.0, 3, 0)
+        ep = DeviceFtEpisodes(eng, [cfg], vg, bg, rmm.L, rmm.delta_t, rmm.eps, "rect+rot")
+        ep.run(3)
+        calls, stop, _ = ep.read_progress()
+        assert calls[0] == 1 and stop[0] & MPC_EP_NO_TRAJ
+    finally:
+        rmm.configure()
+
+
 def test_tree_episode_loop_batched_equals_sequential(engine):
     """run_math_model.py's episode loop over the tree expansion (the named
     entry at config.py's resolution, SURVEY Fact 2): R episodes in lockstep

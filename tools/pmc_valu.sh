@@ -11,7 +11,9 @@ CNT="SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL
 for spec in "chain|1000000 10 chain 20 4|k_episode_chain|160e6" \
             "qk21|1000000 10 qk21 20 4|k_rollout_argmin_stream|160e6" \
             "gen|1000000 10 generated 20 1|k_rollout_generated|0" \
-            "ft|0 0 fulltree 6 1|k_ft_leaves|0"; do
+            "ft|0 0 fulltree 6 1|k_ft_leaves|0" \
+            "episodes_R|1000 1000 tree_episodes 1 1|k_episodes_run|0" \
+            "ftepisodes_G|1000 50 ft_episodes 1 1|k_ft_episodes_run|0"; do
   IFS='|' read name args kern algo <<< "$spec"
   mkdir -p $OUT/$name
   timeout -k 10 120 rocprofv3 --pmc $CNT --output-format csv -d $OUT/$name/pmc1 -o p -- python3 tools/prof_kernel.py $args > $OUT/$name/pmc1.log 2>&1 || { echo "$name failed"; tail -5 $OUT/$name/pmc1.log; exit 1; }
@@ -19,7 +21,7 @@ for spec in "chain|1000000 10 chain 20 4|k_episode_chain|160e6" \
 done
 python3 - <<PY
 import json
-for n in ("chain", "qk21", "gen", "ft"):
+for n in ("chain", "qk21", "gen", "ft", "episodes_R", "ftepisodes_G"):
     d = json.load(open("$OUT/%s.json" % n))
     c = d["counters_median_per_launch"]
     print(n, d["kernel"], "fp64 ops/launch %.4g" % (d["fp64_ops_per_launch"] or 0),

@@ -11,7 +11,9 @@ the RCCL all_gather, over a 1-rank nccl group: the N > 1 bench's launch);
 N > 1 bench's launch);
 "generated": generated-controls episode steps (k_rollout_generated, rect+cum);
 "fulltree": config F's full-tree MPC steps (k_ft_leaves, S1 = 451, n_cand and
-n_steps ignored)."""
+n_steps ignored);
+"tree_episodes" / "ft_episodes": workload R / G's one-launch episode runs
+(n_cand = episodes, n_steps = max_calls)."""
 import os
 import sys
 
@@ -43,6 +45,24 @@ def main():
             rmm.x, rmm.y, rmm.phi, rmm.v, rmm.beta = c
         torch.cuda.synchronize()
         print("done fulltree", reps)
+        return
+    if integ in ("tree_episodes", "ft_episodes"):
+        # workload R / G as bench.py runs them: n = episodes, ns = max_calls
+        from diplomjourney_amd import run_math_model as rmm
+        starts = rmm.draw_starts(n, seed=20261015)
+        for _ in range(reps):
+            if integ == "tree_episodes":
+                from diplomjourney_amd.episode import DeviceEpisodes, tree_episode_config
+                eps = DeviceEpisodes(eng, [tree_episode_config(s, ns) for s in starts], 3, "qk21",
+                                     log_capacity=ns)
+                eps.run(ns)
+            else:
+                import math
+                rmm.INTEGRATOR = "rect+rot"
+                rmm.configure(0.25, math.radians(10))
+                rmm.run_batched(starts, max_calls=ns)
+        torch.cuda.synchronize()
+        print("done", integ, n, ns, reps)
         return
     if integ == "generated":
         from diplomjourney_amd.episode import DeviceEpisode
