@@ -1431,20 +1431,27 @@ def bench_episodes(args, wl, eng, rank, world, cpu):
     s1 = int(rmm.size_max_1)
     starts = rmm.draw_starts(wl["robots"], seed=20261015)
     lo, hi = shard_range(len(starts), rank, world)
+    from diplomjourney_amd.abi import MPC_EP_ARRIVED, MPC_EP_BREAK
+    eps_dev = rmm.device_ft_episodes(starts[lo:hi], args.steps, args.integrator,
+                                     log_capacity=args.steps)
     for _ in range(max(1, args.warmup // 20)):                           # warmup: whole runs
-        rmm.run_batched(starts[lo:hi], max_calls=args.steps)
+        eps_dev.reset()
+        eps_dev.run(args.steps)
+    eps_dev.reset()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    stats = {}
     t0 = time.perf_counter()
-    outs = rmm.run_batched(starts[lo:hi], max_calls=args.steps, stats=stats)
+    eps_dev.run(args.steps)                  # ONE launch: every call of every episode
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    robot_steps = sum(len(r) for r, _ in outs)
-    t = torch.tensor([elapsed, robot_steps, stats["steps"]], dtype=torch.float64,
+    calls, stop, _ = eps_dev.read_progress()
+    outs = [(None, "recursive_error" if st & MPC_EP_BREAK else
+             "on_target" if st & MPC_EP_ARRIVED else "max_calls") for st in stop]
+    robot_steps = int(calls.sum())
+    t = torch.tensor([elapsed, robot_steps, int(calls.max())], dtype=torch.float64,
                      device=eng.device)
     if world > 1:
         mx = t[[0, 2]].clone()
@@ -1469,8 +1476,8 @@ def bench_episodes(args, wl, eng, rank, world, cpu):
                    "episode_loop": "device-resident: one block per robot, one launch for all "
                                    "calls (mpc_fulltree_episodes_run)",
                    "parallelism": f"robot-sharded x{world}, no exchange"},
-        "p50_note": "ms_per_step = the run's time (host, incl. the log read-back) / the "
-                    "longest episode's calls",
+        "p50_note": "ms_per_step = the run's time (one launch + sync) / the longest "
+                    "episode's calls",
         "roofline": {"bound": "valu-fp64", "achieved": flops / 1e12,
                      "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": flops / 1e12 / FP64_VECTOR_PEAK_TFLOPS, "traffic": None,

@@ -134,7 +134,10 @@ __global__ __launch_bounds__(kBlock, kFtEpWaves) void k_ft_episodes_run(
       }
       s_ctl[k] = u;
     }
-    const bool rot = ROT && !__syncthreads_or(wide);
+    // (the barrier that publishes the table: evaluated in every instantiation,
+    // not short-circuited away by a false ROT)
+    const bool any_wide = __syncthreads_or(wide);
+    const bool rot = ROT && !any_wide;
     uint64_t best_k = ~0ull;
     int64_t best_i = INT64_MAX;
     if (rot)

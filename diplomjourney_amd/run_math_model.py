@@ -250,23 +250,15 @@ def run_batched(starts, max_calls=None, integrator=None, chunk=256, stats=None):
     call, ret, optimal_criterion after it); raises the script's TypeError if an
     episode's first call finds no winner.  stats (optional dict) receives the
     lockstep-equivalent steps (the longest episode's calls) and the leaves."""
-    import numpy as np
-    from .abi import (MPC_EP_ARRIVED, MPC_EP_BREAK, MPC_EP_NO_TRAJ, MpcFulltreeEpisodeConfig)
-    from .episode import DeviceFtEpisodes
-    eng, (vg, bg) = _device()
-    integ = INTEGRATOR if integrator is None else integrator
+    from .abi import MPC_EP_ARRIVED, MPC_EP_BREAK, MPC_EP_NO_TRAJ
     robots = [_Robot(s) for s in starts]
-    cfgs = [MpcFulltreeEpisodeConfig(float(r.x_0), float(r.y_0), float(r.phi_0), float(r.x_t),
-                                     float(r.y_t), r.atan_t, float(r.crit), int(max_calls or 0), 0)
-            for r in robots]
     cap = min(chunk, max_calls) if max_calls else chunk
-    eps_dev = DeviceFtEpisodes(eng, cfgs, vg, bg, float(L), float(delta_t), float(eps), integ,
-                               log_capacity=cap)
+    eps_dev = device_ft_episodes(starts, max_calls, integrator, cap, robots)
     logs = [[] for _ in robots]
     while True:
         eps_dev.run(cap)
         for r, lg in enumerate(eps_dev.read_logs(first_step=[len(x) for x in logs])):
-            logs[r].extend(lg)
+            logs[r].extend(lg[["x", "y", "phi", "v", "beta", "cost"]].tolist())
         calls, stop, leaves = eps_dev.read_progress()
         if (stop != 0).all():
             break
@@ -280,15 +272,31 @@ def run_batched(starts, max_calls=None, integrator=None, chunk=256, stats=None):
         recs = []
         x, y, phi, v, t, crit = r.x, r.y, r.phi, r.v, r.t, r.crit
         for g in lg:
-            ret = [float(g["x"]), float(g["y"]), float(g["phi"]), float(g["v"]), float(g["beta"])]
+            ret = list(g[:5])                                 # x, y, phi, v, beta
             recs.append({"pre": (x, y, phi, v, t, crit), "ret": ret,
-                         "optimal_criterion": float(g["cost"])})
+                         "optimal_criterion": g[5]})
             x, y, phi, v = ret[:4]
             t = t + delta_t
-            crit = float(g["cost"])
+            crit = g[5]
         out.append((recs, "recursive_error" if st & MPC_EP_BREAK else
                     "on_target" if st & MPC_EP_ARRIVED else "max_calls"))
     return out
+
+
+def device_ft_episodes(starts, max_calls=None, integrator=None, log_capacity=256, robots=None):
+    """The device state of len(starts) full-tree episodes (episode.DeviceFtEpisodes)
+    with the script's grids, constants and first incumbents: run_batched's
+    engine, also driven directly by bench.py's workload G."""
+    from .abi import MpcFulltreeEpisodeConfig
+    from .episode import DeviceFtEpisodes
+    eng, (vg, bg) = _device()
+    integ = INTEGRATOR if integrator is None else integrator
+    robots = robots or [_Robot(s) for s in starts]
+    cfgs = [MpcFulltreeEpisodeConfig(float(r.x_0), float(r.y_0), float(r.phi_0), float(r.x_t),
+                                     float(r.y_t), r.atan_t, float(r.crit), int(max_calls or 0), 0)
+            for r in robots]
+    return DeviceFtEpisodes(eng, cfgs, vg, bg, float(L), float(delta_t), float(eps), integ,
+                            log_capacity=log_capacity)
 
 
 def run_batched_lockstep(starts, max_calls=None, integrator=None):
