@@ -119,6 +119,10 @@ def parse():
                          "input); sampled: the device sampler regenerates them per step")
     ap.add_argument("--no-second-pass", action="store_true",
                     help="skip the comparison run with the other --inputs mode")
+    ap.add_argument("--layout", default="tiled", choices=["tiled", "soa"],
+                    help="resident batches of the chained steps (one GPU, P2P): tiled = "
+                         "MPC_LAYOUT_TILED (each 512-candidate tile's horizon contiguous in HBM, "
+                         "include/mpc_rollout.h), soa = the step-major SoA every entry accepts")
     ap.add_argument("--no-config-d", action="store_true",
                     help="workload C: skip the config-D sub-result (N=12, 1.25e6 candidates "
                          "per GPU, the BASELINE multi-GPU config) measured in the same run")
@@ -534,7 +538,10 @@ def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
                            generate=inputs == "generated",
                            overlap=overlap, p2p=p2p)
         p2p = bool(getattr(ep, "p2p", False))    # (False if its self-test failed)
-    pool = make_pool(eng, ep, n_steps, args.steps) if inputs == "resident" else None
+    # the chained steps stream tiled batches (one GPU and P2P forms)
+    tiled = (args.layout == "tiled" and inputs == "resident" and not args.host_loop
+             and getattr(ep, "chain", False) and (not exchange or p2p))
+    pool = make_pool(eng, ep, n_steps, args.steps, tiled) if inputs == "resident" else None
     rollout_ms = None
     # the launch that carries the step: the chained kernel (rollout of step k +
     # completion of step k-1; on G > 1 its exchange form, which also selects
@@ -551,7 +558,7 @@ def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
         kern_ms = chain_pass(ep, pool)
         # for comparison: the same controls through the rollout kernel alone
         # (the chained launch adds block 0's completion of the previous step)
-        rollout_ms = None if sub else kernel_pass(ep, pool)
+        rollout_ms = None if sub else kernel_pass(ep, soa_pool(ep, pool))
     elif xchg_chain:
         # P2P: no collective between launches, so back-to-back launches
         # between one pair of events (chain_pass); the all_gather form has its
@@ -630,6 +637,8 @@ def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
         "config": {"workload": wl["desc"], "n_steps": n_steps,
                    "candidates_per_gpu": ep.n_local, "candidates_total": n_total,
                    "integrator": args.integrator, "inputs": INPUTS_DOC[inputs],
+                   "layout": (LAYOUT_DOC["tiled"] if tiled else LAYOUT_DOC["soa"])
+                   if inputs == "resident" else None,
                    "episodes_started": episodes,
                    "episode_loop": "host" if args.host_loop else "device-resident",
                    "launch": (("hipGraph of the K steps" + (" incl. the RCCL all_gather"
@@ -669,7 +678,8 @@ def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
         "chain_error": chain_err,
         "kernel_ms": kern_ms, "kernel_in_step_ms": main_run["kernel_in_step_ms"],
         "roofline": (None if inputs == "generated" else
-                     roofline(achieved, bytes_launch, args.traffic_json, kernel=kernel)),
+                     roofline(achieved, bytes_launch, args.traffic_json, kernel=kernel,
+                              layout="tiled" if tiled else "soa")),
         "roofline_rollout_only": (None if rollout_ms is None else
                                   roofline(bytes_launch / (rollout_ms * 1e-3) / 1e9, bytes_launch,
                                            None, kernel="k_rollout_argmin_stream")),
@@ -730,7 +740,7 @@ def parity_pass(args, eng, ep, pool, rank, world, device):
     with ThreadPoolExecutor(max_workers=threads) as ex:
         futs = []
         for i in range(K):
-            vh, bh = (a.cpu().numpy() for a in pool[i])
+            vh, bh = (a.cpu().numpy() for a in soa_pool(fresh, pool[i:i + 1])[0])
             futs.append(ex.submit(O.rollout_argmin, probs[i][0], vh, bh, index_base=fresh.lo,
                                   incumbent=probs[i][1], integ="qk21", want_costs=True))
         for i, f in enumerate(futs):
@@ -794,7 +804,8 @@ def finish(ep, have_group):
 def stream_ceiling(ep, pool, reps=100, warm=100):
     """Measured read ceiling of the rollout's own access pattern on this GPU:
     mpc_stream_probe (the streaming kernel's grid, tiles and LDS-DMA control
-    ring, no arithmetic) over the same resident batches, REPS back-to-back
+    ring, no arithmetic; mpc_stream_probe_tiled for tiled batches) over the
+    same resident batches, REPS back-to-back
     launches between HIP events on the episode's stream, rotating over the
     pool as kernel_pass does.  Returns (GB/s of the 16 B per candidate-step
     read, ms per launch)."""
@@ -806,9 +817,14 @@ def stream_ceiling(ep, pool, reps=100, warm=100):
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     def one(i):
-        v, b = pool[i % len(pool)]
-        rc = lib.mpc_stream_probe(v.data_ptr(), b.data_ptr(), n, ns, sink.data_ptr(),
-                                  sink.numel() * 8, st)
+        p = pool[i % len(pool)]
+        if isinstance(p, torch.Tensor):      # tiled: the chained kernel's tiled pattern
+            rc = lib.mpc_stream_probe_tiled(p.data_ptr(), n, ns, sink.data_ptr(),
+                                            sink.numel() * 8, st)
+        else:
+            v, b = p
+            rc = lib.mpc_stream_probe(v.data_ptr(), b.data_ptr(), n, ns, sink.data_ptr(),
+                                      sink.numel() * 8, st)
         if rc != 0:
             raise RuntimeError(f"mpc_stream_probe: status {rc}")
     for i in range(warm):
@@ -877,20 +893,42 @@ INPUTS_DOC = {
 }
 
 
-def make_pool(eng, ep, n_steps, k):
+def make_pool(eng, ep, n_steps, k, tiled=False):
     """Distinct resident candidate batches for the timed steps (cycled when
     K batches would exceed ~16 GB; at least 4, so a batch is never
-    cache-resident when it comes round again)."""
+    cache-resident when it comes round again).  tiled: MPC_LAYOUT_TILED
+    tensors (the same candidates as the SoA batches of the same seeds)."""
     import torch
     from diplomjourney_amd import math_model_tree as mmt
     batch = 16 * n_steps * ep.n_local
     n = max(1, min(k, max(4, int(16e9 // batch))))
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device=eng.device)
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device=eng.device)
-    pool = [eng.sample_controls(V, B, ep.n_local, n_steps, 0x5EED0000 + i, index_base=ep.lo)
-            for i in range(n)]
+    if tiled:
+        pool = [eng.sample_controls_tiled(V, B, ep.n_local, n_steps, 0x5EED0000 + i,
+                                          index_base=ep.lo) for i in range(n)]
+    else:
+        pool = [eng.sample_controls(V, B, ep.n_local, n_steps, 0x5EED0000 + i, index_base=ep.lo)
+                for i in range(n)]
     torch.cuda.synchronize()
     return pool
+
+
+def soa_pool(ep, pool, k=4):
+    """The first k batches as SoA (v, beta) pairs (tiled batches converted):
+    for the passes that read the ABI's step-major layout (the streaming kernel
+    alone, the host checker)."""
+    import torch
+    from diplomjourney_amd.expansion import tiled_to_soa
+    out = [tiled_to_soa(p, ep.n_local) if isinstance(p, torch.Tensor) else p for p in pool[:k]]
+    return out
+
+
+LAYOUT_DOC = {
+    "tiled": "MPC_LAYOUT_TILED: each 512-candidate tile's v and beta of every step in one "
+             "contiguous run (include/mpc_rollout.h); 16 B per candidate-step as in SoA",
+    "soa": "step-major SoA v_sc[s * C + c], beta_sc[s * C + c]",
+}
 
 
 def run_steps(args, ep, pool, use_graph, world, device):
@@ -1046,15 +1084,20 @@ P2P_KERNEL = "k_episode_chain[p2p]"
 # one per measured size; the one whose algorithmic bytes match is used
 TRAFFIC_JSON = {"k_rollout_argmin_stream": ["r03_traffic_stream.json"],
                 "k_episode_chain": ["r04_final/close/traffic_chain.json",
-                                    "r05/traffic_chain_D.json"],
+                                    "r05/traffic_chain_D.json",
+                                    "r05/traffic_chain_tiled.json",
+                                    "r05/traffic_chain_tiled_D.json"],
                 XCHG_KERNEL: ["r04/traffic_chain_xchg.json"],
                 P2P_KERNEL: ["r04_final/close/traffic_chain_p2p.json",
-                             "r05/traffic_chain_p2p_D.json"]}
+                             "r05/traffic_chain_p2p_D.json",
+                             "r05/traffic_chain_p2p_tiled.json",
+                             "r05/traffic_chain_p2p_tiled_D.json"]}
 
 
-def traffic_summary(traffic_json, kernel, bytes_launch):
+def traffic_summary(traffic_json, kernel, bytes_launch, layout="soa"):
     """(summary dict, path) of the PMC summary measured on this kernel at this
-    algorithmic size (traffic_json: an explicit file), else (None, None)."""
+    algorithmic size and control layout (traffic_json: an explicit file), else
+    (None, None)."""
     paths = ([traffic_json] if traffic_json else
              [os.path.join(REPO, "profiles", p) for p in TRAFFIC_JSON.get(kernel, [])])
     for path in paths:
@@ -1063,7 +1106,7 @@ def traffic_summary(traffic_json, kernel, bytes_launch):
         with open(path) as fh:
             t = json.load(fh)
         if (abs(t.get("algorithmic_bytes_per_launch", -1) - bytes_launch) < 1
-                and t.get("kernel", kernel) == kernel):
+                and t.get("kernel", kernel) == kernel and t.get("layout", "soa") == layout):
             return t, path
     return None, None
 
@@ -1132,16 +1175,17 @@ def chain_pass(ep, pool, reps=100, warm=200):
     return k0.elapsed_time(k1) / reps
 
 
-def roofline(achieved, bytes_launch, traffic_json, kernel="k_rollout_argmin_stream"):
+def roofline(achieved, bytes_launch, traffic_json, kernel="k_rollout_argmin_stream",
+             layout="soa"):
     """traffic: HBM bytes per launch from the committed PMC summary, used only
-    when it was measured on the same kernel at the same algorithmic size."""
+    when it was measured on the same kernel, algorithmic size and layout."""
     traffic, src = None, None
-    t, path = traffic_summary(traffic_json, kernel, bytes_launch)
+    t, path = traffic_summary(traffic_json, kernel, bytes_launch, layout)
     if t:
         traffic, src = t.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
-            "kernel": kernel, "algorithmic_bytes_per_launch": bytes_launch}
+            "kernel": kernel, "layout": layout, "algorithmic_bytes_per_launch": bytes_launch}
 
 
 def bench_robots(args, wl, eng, rank, world, cpu):

@@ -22,6 +22,12 @@ MPC_HEADING_CUMULATIVE = 0x200
 
 # integrator argument of the C ABI: QUADPACK-exact or exact integral, each
 # with the heading evaluated directly (reference formula) or by rotation
+# control layout flag OR'ed into the integrator of the chained / P2P entries
+# (include/mpc_rollout.h MPC_LAYOUT_TILED): tile t of MPC_TILE candidates holds
+# per step its MPC_TILE v values then its MPC_TILE beta values
+MPC_LAYOUT_TILED = 0x400
+MPC_TILE = 512
+
 INTEGRATORS = {"qk21": MPC_INTEG_QK21, "rect": MPC_INTEG_RECT,
                "qk21+rot": MPC_INTEG_QK21 | MPC_HEADING_ROTATE,
                "rect+rot": MPC_INTEG_RECT | MPC_HEADING_ROTATE,

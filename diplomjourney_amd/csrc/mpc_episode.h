@@ -1002,6 +1002,7 @@ __device__ __forceinline__ mpc_candidate_t* cand_lds() {
 // and its controls — into `out` (LDS).  Each wave loads its own best's
 // controls while the waves' minima are combined (finalize_block's prefetch:
 // no dependent load after the block's winner is known).
+template <bool TILED = false>
 __device__ void records_candidate(const Rec* __restrict__ part, int n_part,
                                   const double* __restrict__ v, const double* __restrict__ b,
                                   int64_t n_cand, int n_steps, int64_t index_base,
@@ -1025,8 +1026,9 @@ __device__ void records_candidate(const Rec* __restrict__ part, int n_part,
   const int ln = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double pv = 0.0, pb = 0.0;
   if (k != ~0ull && ln < n_steps) {
-    pv = v[ln * n_cand + i];
-    pb = b[ln * n_cand + i];
+    const int64_t o = ctl_off<TILED>(ln, i, TILED ? n_steps : n_cand);
+    pv = v[o];
+    pb = b[o];
   }
   __shared__ uint64_t s_k[kWaves];
   __shared__ int64_t s_i[kWaves];
@@ -1130,7 +1132,7 @@ __device__ const mpc_candidate_t* wait_mailbox(EpisodeState* S, void* mb, uint32
 // rank's candidate from the previous launch's records, posted; the world
 // candidates awaited; the global winner re-rolled into out_prev and the
 // episode updated, publishing `publish_epoch` (0: end of the chain).
-template <int INTEG, int ROT>
+template <int INTEG, int ROT, bool TILED = false>
 __device__ void p2p_complete(const mpc_episode_config_t& c, EpisodeState* S, void* mb, int world,
                              uint32_t prev, const Rec* __restrict__ part_prev, int n_part_prev,
                              const double* __restrict__ v_prev, const double* __restrict__ b_prev,
@@ -1150,7 +1152,8 @@ __device__ void p2p_complete(const mpc_episode_config_t& c, EpisodeState* S, voi
   const uint32_t prior_err = threadIdx.x == 0 ? S->chain_error : 0u;
   const uint32_t seq = threadIdx.x == 0 ? S->p2p_seq : 0u;
   mpc_candidate_t* lc = cand_lds();
-  records_candidate(part_prev, n_part_prev, v_prev, b_prev, n_cand, n_steps, index_base, lc);
+  records_candidate<TILED>(part_prev, n_part_prev, v_prev, b_prev, n_cand, n_steps, index_base,
+                           lc);
   if (static_cast<int>(threadIdx.x) < world) s_peers[threadIdx.x] = my_peer;
   if (threadIdx.x == 0) {
     s_rank = my_rank;
@@ -1196,13 +1199,13 @@ __global__ __launch_bounds__(64) void k_mailbox_ping(void* mb, uint32_t tag, int
   if (r == 0) ok[0] = all ? 1 : 0;
 }
 
-template <int INTEG, int ROT>
+template <int INTEG, int ROT, bool TILED>
 __global__ __launch_bounds__(kBlock) void k_episode_p2p_flush(
     mpc_episode_config_t c, EpisodeState* __restrict__ S, void* mailbox, uint32_t tag, int world,
     const Rec* __restrict__ part, int n_part, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, int64_t index_base,
     mpc_result_t* __restrict__ out, mpc_episode_log_t* __restrict__ log, int cap) {
-  p2p_complete<INTEG, ROT>(c, S, mailbox, world, tag, part, n_part, v, b, n_cand, n_steps,
+  p2p_complete<INTEG, ROT, TILED>(c, S, mailbox, world, tag, part, n_part, v, b, n_cand, n_steps,
                            index_base, out, log, cap, 0u);
 }
 
@@ -1226,7 +1229,7 @@ constexpr int chain_waves() {
 // form, whose records block 0 of the SAME launch collects).  WAIT_TICKS bounds
 // the wait for block 0's constants (kChainWaitTicks on one GPU,
 // kXchgWaitTicks when block 0 itself waits for peers or a collective).
-template <int INTEG, int ROT, bool PL2, bool TAGGED, uint64_t WAIT_TICKS>
+template <int INTEG, int ROT, bool PL2, bool TAGGED, uint64_t WAIT_TICKS, bool TILED>
 __device__ __forceinline__ void chain_tiles(EpisodeState* __restrict__ S, uint32_t epoch,
                                             const double* __restrict__ v,
                                             const double* __restrict__ b, int64_t n_cand,
@@ -1327,8 +1330,12 @@ __device__ __forceinline__ void chain_tiles(EpisodeState* __restrict__ S, uint32
     double cst[CPL];
     // leading trig coefficients not pinned: the fifth wave per SIMD needs the
     // registers more (as the rect+cum stream kernel)
+    // TILED: the tile's rows are one contiguous run (tile base + s * 1024
+    // doubles), the lane's column its offset within the tile
+    const int64_t tb0 = TILED ? static_cast<int64_t>(tile) * (2 * MPC_TILE) * n_steps : 0;
     rollout_lane_glds_k<INTEG, ROT, PL2, decltype(wait), decltype(pre0), decltype(mid),
-                        false>(K, Kl, v, b, n_cand, cl, n_steps, cst, wait, pre0, mid);
+                        false>(K, Kl, v + tb0, b + tb0, TILED ? 2 * MPC_TILE : n_cand,
+                               TILED ? cl - tile * MPC_TILE : cl, n_steps, cst, wait, pre0, mid);
     if (c0 < n32) {
 #pragma unroll
       for (int j = 0; j < CPL; ++j) {
@@ -1349,7 +1356,7 @@ __device__ __forceinline__ void chain_tiles(EpisodeState* __restrict__ S, uint32
   }
 }
 
-template <int INTEG, int ROT, int MODE, bool PL2>
+template <int INTEG, int ROT, int MODE, bool PL2, bool TILED = false>
 __global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
     EpisodeState* __restrict__ S, uint32_t epoch, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, Rec* __restrict__ part,
@@ -1368,17 +1375,16 @@ __global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
         // every mailbox; the world's awaited; selection and update.
         // (`gathered` carries the mailbox, n_gathered the world size, wait_tag
         // the previous step's epoch)
-        p2p_complete<INTEG, ROT>(ecfg, S, const_cast<mpc_candidate_t*>(gathered), n_gathered,
+        p2p_complete<INTEG, ROT, TILED>(ecfg, S, const_cast<mpc_candidate_t*>(gathered), n_gathered,
                                  wait_tag, part_prev, n_part_prev, v_prev, b_prev, n_cand,
                                  n_steps, index_base, out_prev, log, cap, epoch);
       } else if constexpr (MODE == kChainFin) {
         const Consts Kp = S->h.K;
         const EpisodeHook hook{&S->h, log, cap, S->chain_pub, kPubWords, epoch};
         // (block 0 never fills the control ring: its LDS holds the re-roll)
-        finalize_block<INTEG, ROT, true, kBlock, false>(part_prev, n_part_prev, Kp, v_prev,
-                                                        b_prev, n_cand, n_steps, index_base,
-                                                        S->h.incumbent, out_prev, ecfg, hook,
-                                                        ring_lds());
+        finalize_block<INTEG, ROT, true, kBlock, false, false, TILED>(
+            part_prev, n_part_prev, Kp, v_prev, b_prev, n_cand, n_steps, index_base,
+            S->h.incumbent, out_prev, ecfg, hook, ring_lds());
       } else {
         // overlapped exchange: the gathered candidates come from a collective
         // that ran beside this launch — wait for its mark, stage them in LDS.
@@ -1410,9 +1416,10 @@ __global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
                               &S->chain_error);
     return;
   }
+  static_assert(!TILED || MODE != kChainXchg, "the all_gather form reads SoA controls");
   chain_tiles<INTEG, ROT, PL2, MODE == kChainXchg,
-              MODE == kChainFin ? kChainWaitTicks : kXchgWaitTicks>(S, epoch, v, b, n_cand,
-                                                                    n_steps, part, has_prev, ecfg);
+              MODE == kChainFin ? kChainWaitTicks : kXchgWaitTicks, TILED>(
+      S, epoch, v, b, n_cand, n_steps, part, has_prev, ecfg);
 }
 
 }  // namespace mpc

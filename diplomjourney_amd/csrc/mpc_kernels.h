@@ -42,6 +42,18 @@ struct Rec {
   int64_t idx;
 };
 
+// Offset of candidate c's control at step s: step-major SoA (pitch = the row
+// pitch ld) or TILED (MPC_LAYOUT_TILED, pitch = n_steps: tile c / 512 holds
+// per step 512 v then 512 beta; the beta pointer is the v pointer + 512).
+template <bool TILED>
+__host__ __device__ __forceinline__ int64_t ctl_off(int64_t s, int64_t c, int64_t pitch) {
+  if constexpr (TILED)
+    return (c >> 9) * (pitch << 10) + (s << 10) + (c & 511);
+  else
+    return s * pitch + c;
+}
+static_assert(MPC_TILE == 512, "ctl_off's shifts");
+
 // Block-level arg-min: wave shuffle, then the kWaves wave records via LDS.
 // The block winner ends up in thread 0.
 // IDX31: every index is below 2^31 (wave_argmin32).
@@ -517,6 +529,9 @@ __global__ __launch_bounds__(kBlock, kStreamWaves) void k_rollout_argmin_stream(
 // read-only stream ceiling of the rollout's own access pattern at the
 // launch's size (launch ramp and tail included), the denominator the
 // streaming kernels' time is compared with.
+// TILED: the same over MPC_LAYOUT_TILED controls (a tile's rows at tile base +
+// s * 1024 doubles, the lane's offset within its tile).
+template <bool TILED>
 __global__ __launch_bounds__(kBlock, kStreamWaves) void k_stream_probe(
     const double* __restrict__ v, const double* __restrict__ b, int64_t n_cand, int n_steps,
     uint64_t* __restrict__ sink) {
@@ -531,10 +546,13 @@ __global__ __launch_bounds__(kBlock, kStreamWaves) void k_stream_probe(
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     const int64_t c0 = tile * (kBlock * 2) + threadIdx.x * 2;
     if (c0 >= n_cand) continue;   // n_cand even (host check): the pair is valid
-    const uint32_t voff = static_cast<uint32_t>(c0) * 8u;
+    const int64_t ld = TILED ? 2 * MPC_TILE : n_cand;   // row pitch
+    const double* tv = TILED ? v + tile * ld * n_steps : v;
+    const double* tb = TILED ? b + tile * ld * n_steps : b;
+    const uint32_t voff = static_cast<uint32_t>(TILED ? c0 - tile * MPC_TILE : c0) * 8u;
 #pragma unroll
     for (int u = 0; u < R - 1; ++u)
-      if (u < n_steps) glds_pair(v + u * n_cand, b + u * n_cand, voff, dst(u), dst(u) + kSlot / 2);
+      if (u < n_steps) glds_pair(tv + u * ld, tb + u * ld, voff, dst(u), dst(u) + kSlot / 2);
     double2 v2 = make_double2(0.0, 0.0), b2 = v2;
 #pragma unroll 1
     for (int s = 0; s < n_steps; s += R) {
@@ -544,8 +562,8 @@ __global__ __launch_bounds__(kBlock, kStreamWaves) void k_stream_probe(
         if (st < n_steps) {
           if (st + R - 1 < n_steps) {
             const int sr = st + R - 1, slot = (u + R - 1) % R;
-            glds_refill(v + sr * n_cand, b + sr * n_cand, voff, dst(slot), dst(slot) + kSlot / 2,
-                        v2, b2);
+            glds_refill(tv + sr * ld, tb + sr * ld, voff, dst(slot), dst(slot) + kSlot / 2, v2,
+                        b2);
             wait_vm<2 * (R - 1)>();
           } else {
             wait_vm<0>();
@@ -944,7 +962,7 @@ __device__ __forceinline__ void load8_rec_sc1_sbase(const Rec* base, const uint3
 // GEN (generated controls, k_rollout_generated): v / b are [n_part][MPC_MAX_STEPS]
 // — the controls of each rollout block's best candidate — instead of the
 // [n_steps][n_cand] candidate arrays; the winner's are those of its block.
-template <int INTEG, int ROT, bool KDEV, int NT, bool SC1, bool GEN = false>
+template <int INTEG, int ROT, bool KDEV, int NT, bool SC1, bool GEN = false, bool TILED = false>
 __device__ __forceinline__ void finalize_block(
     const Rec* __restrict__ part, int n_part, const Consts& K, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, int64_t index_base,
@@ -1012,8 +1030,9 @@ __device__ __forceinline__ void finalize_block(
   const int ln = threadIdx.x & 63;
   if constexpr (!GEN) {
     if (k != ~0ull && ln < n_steps) {
-      pv = v[ln * n_cand + i];
-      pb = b[ln * n_cand + i];
+      const int64_t o = ctl_off<TILED>(ln, i, TILED ? n_steps : n_cand);
+      pv = v[o];
+      pb = b[o];
     }
   }
   if (ln == 0) {
@@ -1079,7 +1098,7 @@ __global__ __launch_bounds__(kFinBlock) void k_finalize_gen(
                                                            out, ecfg, hook, &lds);
 }
 
-template <int INTEG, int ROT, bool KDEV>
+template <int INTEG, int ROT, bool KDEV, bool TILED = false>
 __global__ __launch_bounds__(kFinBlock) void k_finalize(
     const Rec* __restrict__ part, int n_part, Consts Karg, const Consts* __restrict__ Kdev,
     const double* __restrict__ v, const double* __restrict__ b, int64_t n_cand, int n_steps,
@@ -1088,8 +1107,8 @@ __global__ __launch_bounds__(kFinBlock) void k_finalize(
   const Consts K = KDEV ? *Kdev : Karg;
   const double incumbent = KDEV ? *incumbent_dev : incumbent_arg;
   __shared__ EmitLds lds;
-  finalize_block<INTEG, ROT, KDEV, kFinBlock, false>(part, n_part, K, v, b, n_cand, n_steps,
-                                                     index_base, incumbent, out, ecfg, hook, &lds);
+  finalize_block<INTEG, ROT, KDEV, kFinBlock, false, false, TILED>(
+      part, n_part, K, v, b, n_cand, n_steps, index_base, incumbent, out, ecfg, hook, &lds);
 }
 
 // Device-resident episode, one launch per MPC step: the streaming rollout +
@@ -1279,9 +1298,11 @@ constexpr int kSampleLdsEntries = 2048;  // expanded (v, beta) grid staged in LD
 // ds_read_b128 instead of a division by |B| and two loads.
 // cprefix 2 (the episode's enumeration mode): candidates past the grid are
 // padding — NaN controls, a NaN cost, never chosen.
+// tiled: v / b are the MPC_LAYOUT_TILED buffer's base and base + 512, ld its
+// n_steps (ctl_off).
 __device__ void sample_items(const double2* s_grid, uint32_t n_grid, int64_t n_cand, int n_steps,
                              uint64_t seed, int64_t base, int cprefix, double* __restrict__ v,
-                             double* __restrict__ b, int64_t ld, int pairs) {
+                             double* __restrict__ b, int64_t ld, int pairs, int tiled = 0) {
   const int cpt = pairs ? 2 : 1;
   const int64_t n_items = n_cand / cpt;
   for (int64_t it = blockIdx.x * static_cast<int64_t>(kBlock) + threadIdx.x; it < n_items;
@@ -1296,8 +1317,9 @@ __device__ void sample_items(const double2* s_grid, uint32_t n_grid, int64_t n_c
         const double2 e1 = (cprefix == 2 && g + 1 >= n_grid)
                                ? pad
                                : s_grid[grid_entry(seed, st, g + 1, n_grid, cprefix)];
-        *reinterpret_cast<double2*>(v + st * ld + c) = make_double2(e0.x, e1.x);
-        *reinterpret_cast<double2*>(b + st * ld + c) = make_double2(e0.y, e1.y);
+        const int64_t o = tiled ? ctl_off<true>(st, c, ld) : ctl_off<false>(st, c, ld);
+        *reinterpret_cast<double2*>(v + o) = make_double2(e0.x, e1.x);
+        *reinterpret_cast<double2*>(b + o) = make_double2(e0.y, e1.y);
       } else {
         v[st * ld + c] = e0.x;
         b[st * ld + c] = e0.y;
@@ -1309,7 +1331,7 @@ __device__ void sample_items(const double2* s_grid, uint32_t n_grid, int64_t n_c
 __global__ __launch_bounds__(kBlock) void k_sample_controls(
     const double* __restrict__ vg, int nv, const double* __restrict__ bg, int nb, int64_t n_cand,
     int n_steps, uint64_t seed, int64_t base, int cprefix, double* __restrict__ v,
-    double* __restrict__ b, int64_t ld, int pairs) {
+    double* __restrict__ b, int64_t ld, int pairs, int tiled) {
   __shared__ double2 s_grid[kSampleLdsEntries];
   const uint32_t n_grid = static_cast<uint32_t>(nv) * static_cast<uint32_t>(nb);
   if (n_grid > kSampleLdsEntries) {
@@ -1321,8 +1343,9 @@ __global__ __launch_bounds__(kBlock) void k_sample_controls(
       for (int st = 0; st < n_steps; ++st)
         for (int j = 0; j < cpt; ++j) {
           const uint32_t k = grid_entry(seed, st, base + c + j, n_grid, cprefix);
-          v[st * ld + c + j] = vg[k / nb];
-          b[st * ld + c + j] = bg[k % nb];
+          const int64_t o = tiled ? ctl_off<true>(st, c + j, ld) : ctl_off<false>(st, c + j, ld);
+          v[o] = vg[k / nb];
+          b[o] = bg[k % nb];
         }
     }
     return;
@@ -1330,7 +1353,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_controls(
   for (uint32_t k = threadIdx.x; k < n_grid; k += kBlock)
     s_grid[k] = make_double2(vg[k / nb], bg[k % nb]);
   __syncthreads();
-  sample_items(s_grid, n_grid, n_cand, n_steps, seed, base, cprefix, v, b, ld, pairs);
+  sample_items(s_grid, n_grid, n_cand, n_steps, seed, base, cprefix, v, b, ld, pairs, tiled);
 }
 
 }  // namespace mpc

@@ -93,8 +93,10 @@ using BC = std::integral_constant<bool, V>;
 //   -> f(IC<INTEG>, IC<ROT>), ROT 0 direct heading, 1 rotation, 2 (kRotCum)
 //   rotation from the identity with the pose applied last (rect only).
 // allow_cum = false for the full-tree entry points (their own recurrence).
-int mode_ok(int32_t integrator, bool allow_cum = true) {
-  if (integrator & ~(0xff | MPC_HEADING_ROTATE | MPC_HEADING_CUMULATIVE))
+// allow_tiled: the entry accepts MPC_LAYOUT_TILED controls.
+int mode_ok(int32_t integrator, bool allow_cum = true, bool allow_tiled = false) {
+  if (integrator & ~(0xff | MPC_HEADING_ROTATE | MPC_HEADING_CUMULATIVE |
+                     (allow_tiled ? MPC_LAYOUT_TILED : 0)))
     return MPC_ERR_UNSUPPORTED;
   const int integ = integrator & 0xff;
   if (integ != MPC_INTEG_QK21 && integ != MPC_INTEG_RECT) return MPC_ERR_UNSUPPORTED;
@@ -104,6 +106,19 @@ int mode_ok(int32_t integrator, bool allow_cum = true) {
 }
 
 inline bool is_cum(int32_t integrator) { return (integrator & MPC_HEADING_CUMULATIVE) != 0; }
+inline bool is_tiled(int32_t integrator) { return (integrator & MPC_LAYOUT_TILED) != 0; }
+
+// MPC_LAYOUT_TILED controls: v = the buffer's base (16-B aligned), beta =
+// v + 512, n_cand even (two candidates per lane) and below 2^31.
+bool tiled_ok(const double* v, const double* b, int64_t n_cand) {
+  return v && b == v + MPC_TILE && (reinterpret_cast<uintptr_t>(v) & 15) == 0 &&
+         n_cand >= 2 && n_cand % 2 == 0 && n_cand < (int64_t{1} << 31);
+}
+
+// The chained entries' control check: the aligned SoA path or the tiled layout.
+bool chain_ctl_ok(const double* v, const double* b, int64_t n_cand, int32_t integrator) {
+  return is_tiled(integrator) ? tiled_ok(v, b, n_cand) : wide_ok(v, b, n_cand);
+}
 
 template <class F>
 void dispatch_mode(int32_t integrator, F&& f) {
@@ -190,6 +205,14 @@ void launch_finalize(hipStream_t st, int32_t integrator, const Rec* part, int n_
   dispatch_mode(integrator, [&](auto integ, auto rot) {
     constexpr int I = decltype(integ)::value;
     constexpr int R = decltype(rot)::value;
+    if constexpr (KDEV && R == kRotCum) {
+      if (is_tiled(integrator)) {   // the flush of a tiled chained episode
+        k_finalize<I, R, KDEV, true><<<1, kFinBlock, 0, st>>>(
+            part, n_part, K, Kdev, v, b, n_cand, n_steps, index_base, incumbent, incumbent_dev,
+            out, ecfg, hook);
+        return;
+      }
+    }
     k_finalize<I, R, KDEV><<<1, kFinBlock, 0, st>>>(part, n_part, K, Kdev, v, b, n_cand, n_steps,
                                                     index_base, incumbent, incumbent_dev, out,
                                                     ecfg, hook);
@@ -345,8 +368,20 @@ int mpc_stream_probe(const double* v_sc, const double* beta_sc, int64_t n_cand,
   const int64_t grid = rollout_grid<kCplWide>(n_cand);
   if (sink_bytes < static_cast<size_t>(kMaxBlocks) * kBlock * sizeof(uint64_t))
     return MPC_ERR_WORKSPACE;
-  k_stream_probe<<<grid, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+  k_stream_probe<false><<<grid, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
       v_sc, beta_sc, n_cand, n_steps, static_cast<uint64_t*>(sink));
+  return last_hip_status();
+}
+
+int mpc_stream_probe_tiled(const double* tiles, int64_t n_cand, int32_t n_steps, void* sink,
+                           size_t sink_bytes, mpc_stream_t stream) {
+  if (!tiles || n_steps < 1 || n_steps > MPC_MAX_STEPS || !sink) return MPC_ERR_ARG;
+  if (!tiled_ok(tiles, tiles + MPC_TILE, n_cand)) return MPC_ERR_UNSUPPORTED;
+  if (sink_bytes < static_cast<size_t>(kMaxBlocks) * kBlock * sizeof(uint64_t))
+    return MPC_ERR_WORKSPACE;
+  k_stream_probe<true><<<rollout_grid<kCplWide>(n_cand), kBlock, 0,
+                         reinterpret_cast<hipStream_t>(stream)>>>(
+      tiles, tiles + MPC_TILE, n_cand, n_steps, static_cast<uint64_t*>(sink));
   return last_hip_status();
 }
 
@@ -383,7 +418,25 @@ int mpc_sample_controls(const double* v_grid, int32_t n_v, const double* beta_gr
   const int64_t grid = std::min<int64_t>(cdiv(items, kBlock), 4096);
   k_sample_controls<<<grid, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
       v_grid, n_v, beta_grid, n_beta, n_cand, n_steps, seed, index_base, const_prefix, v_sc,
-      beta_sc, ld, pairs);
+      beta_sc, ld, pairs, 0);
+  return last_hip_status();
+}
+
+int mpc_sample_controls_tiled(const double* v_grid, int32_t n_v, const double* beta_grid,
+                              int32_t n_beta, int64_t n_cand, int32_t n_steps, uint64_t seed,
+                              int64_t index_base, int32_t const_prefix, double* tiles,
+                              mpc_stream_t stream) {
+  if (!v_grid || !beta_grid || !tiles || n_v < 1 || n_beta < 1 || n_steps < 1 ||
+      n_steps > MPC_MAX_STEPS || index_base < 0)
+    return MPC_ERR_ARG;
+  if (static_cast<int64_t>(n_v) * n_beta > 0xFFFFFFFFll) return MPC_ERR_ARG;
+  if (!tiled_ok(tiles, tiles + MPC_TILE, n_cand)) return MPC_ERR_ARG;
+  // every slot of every tile, the last tile's padding included
+  const int64_t n_pad = cdiv(n_cand, MPC_TILE) * MPC_TILE;
+  const int64_t grid = std::min<int64_t>(cdiv(n_pad / 2, kBlock), 4096);
+  k_sample_controls<<<grid, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+      v_grid, n_v, beta_grid, n_beta, n_pad, n_steps, seed, index_base, const_prefix, tiles,
+      tiles + MPC_TILE, n_steps, 1, 1);
   return last_hip_status();
 }
 
@@ -494,11 +547,17 @@ int mpc_episode_finalize(void* state, const double* v_sc, const double* beta_sc,
   if (check_episode_arrays(state, v_sc, beta_sc, n_cand, n_steps) != MPC_OK || !out ||
       index_base < 0)
     return MPC_ERR_ARG;
-  if (mode_ok(integrator) != MPC_OK) return MPC_ERR_UNSUPPORTED;
+  if (mode_ok(integrator, true, true) != MPC_OK) return MPC_ERR_UNSUPPORTED;
+  // tiled controls: the flush of a tiled chained episode (its records are the
+  // chained launch's, one per tile)
+  if (is_tiled(integrator) && (!is_cum(integrator) || !advance || !tiled_ok(v_sc, beta_sc, n_cand)))
+    return MPC_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
   if (advance && (check_episode_cfg(advance) != MPC_OK || log_capacity < 0)) return MPC_ERR_ARG;
   EpisodeState* S = static_cast<EpisodeState*>(state);
-  const int n_part = static_cast<int>(partial_count(v_sc, beta_sc, n_cand, false));
+  const int n_part = static_cast<int>(is_tiled(integrator)
+                                          ? rollout_grid<kCplWide>(n_cand)
+                                          : partial_count(v_sc, beta_sc, n_cand, false));
   const mpc_episode_config_t ecfg = advance ? *advance : mpc_episode_config_t{};
   const EpisodeHook hook{advance ? &S->h : nullptr, log, log_capacity,
                          advance ? S->chain_pub : nullptr, advance ? kPubWords : 0};
@@ -564,12 +623,13 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
       check_episode_arrays(state, v_sc, beta_sc, n_cand, n_steps) != MPC_OK || index_base < 0 ||
       log_capacity < 0 || mode != MPC_CHAIN_FINALIZE || epoch == 0)
     return MPC_ERR_ARG;
-  if (mode_ok(integrator) != MPC_OK || !is_cum(integrator) || !wide_ok(v_sc, beta_sc, n_cand))
+  if (mode_ok(integrator, true, true) != MPC_OK || !is_cum(integrator) ||
+      !chain_ctl_ok(v_sc, beta_sc, n_cand, integrator))
     return MPC_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
   int has_prev = 0;
   if (v_prev) {
-    if (!beta_prev || !out_prev || !ws_prev || !wide_ok(v_prev, beta_prev, n_cand))
+    if (!beta_prev || !out_prev || !ws_prev || !chain_ctl_ok(v_prev, beta_prev, n_cand, integrator))
       return MPC_ERR_ARG;
     has_prev = 1;
   }
@@ -582,17 +642,19 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
   // (same n_cand), and as many as mpc_episode_finalize reduces
   const int64_t tiles = rollout_grid<kCplWide>(n_cand);
   const int n_part_prev = static_cast<int>(tiles);
-  auto launch = [&](auto pl2_tag) {
+  auto launch = [&](auto pl2_tag, auto tiled_tag) {
     constexpr bool P = decltype(pl2_tag)::value;
-    k_episode_chain<I, kRotCum, kChainFin, P><<<tiles + 1, kBlock, 0, st>>>(
+    constexpr bool T = decltype(tiled_tag)::value;
+    k_episode_chain<I, kRotCum, kChainFin, P, T><<<tiles + 1, kBlock, 0, st>>>(
         S, epoch, v_sc, beta_sc, n_cand, n_steps, static_cast<Rec*>(ws), has_prev,
         static_cast<const Rec*>(ws_prev), n_part_prev, v_prev, beta_prev, index_base, out_prev,
         nullptr, 0, *cfg, log, log_capacity, 0u);
   };
+  const bool tl = is_tiled(integrator);
   if (pl2)
-    launch(std::true_type{});
+    tl ? launch(std::true_type{}, std::true_type{}) : launch(std::true_type{}, std::false_type{});
   else
-    launch(std::false_type{});
+    tl ? launch(std::false_type{}, std::true_type{}) : launch(std::false_type{}, std::false_type{});
   return last_hip_status();
 }
 
@@ -821,8 +883,9 @@ int mpc_episode_p2p_step(const mpc_episode_config_t* cfg, void* state, uint32_t 
     if (((epoch ^ prev_epoch) & 1u) == 0 || !out_prev || !ws_prev || !v_prev || !beta_prev)
       return MPC_ERR_ARG;
   }
-  if (mode_ok(integrator) != MPC_OK || !is_cum(integrator) || !wide_ok(v_sc, beta_sc, n_cand) ||
-      (prev_epoch && !wide_ok(v_prev, beta_prev, n_cand)))
+  if (mode_ok(integrator, true, true) != MPC_OK || !is_cum(integrator) ||
+      !chain_ctl_ok(v_sc, beta_sc, n_cand, integrator) ||
+      (prev_epoch && !chain_ctl_ok(v_prev, beta_prev, n_cand, integrator)))
     return MPC_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
   EpisodeState* S = static_cast<EpisodeState*>(state);
@@ -834,18 +897,20 @@ int mpc_episode_p2p_step(const mpc_episode_config_t* cfg, void* state, uint32_t 
   constexpr int I = MPC_INTEG_RECT;
   // (the exchange form's argument slots: gathered = this rank's mailbox,
   // n_gathered = world, wait_tag = the previous step's epoch)
-  auto launch = [&](auto pl2_tag) {
+  auto launch = [&](auto pl2_tag, auto tiled_tag) {
     constexpr bool P = decltype(pl2_tag)::value;
-    k_episode_chain<I, kRotCum, kChainP2P, P><<<tiles + 1, kBlock, 0, st>>>(
+    constexpr bool T = decltype(tiled_tag)::value;
+    k_episode_chain<I, kRotCum, kChainP2P, P, T><<<tiles + 1, kBlock, 0, st>>>(
         S, epoch, v_sc, beta_sc, n_cand, n_steps, static_cast<Rec*>(ws), prev_epoch ? 1 : 0,
         static_cast<const Rec*>(ws_prev), static_cast<int>(tiles), v_prev, beta_prev,
         index_base, out_prev, static_cast<const mpc_candidate_t*>(mailbox), world, *cfg, log,
         log_capacity, prev_epoch);
   };
+  const bool tl = is_tiled(integrator);
   if (pl2)
-    launch(std::true_type{});
+    tl ? launch(std::true_type{}, std::true_type{}) : launch(std::true_type{}, std::false_type{});
   else
-    launch(std::false_type{});
+    tl ? launch(std::false_type{}, std::true_type{}) : launch(std::false_type{}, std::false_type{});
   return last_hip_status();
 }
 
@@ -860,14 +925,22 @@ int mpc_episode_p2p_flush(const mpc_episode_config_t* cfg, void* state, uint32_t
       index_base < 0 || !mailbox || last_epoch == 0 || world < 1 || world > kMailMaxRanks ||
       !out || log_capacity < 0 || !ws_last)
     return MPC_ERR_ARG;
-  if (mode_ok(integrator) != MPC_OK || !is_cum(integrator) || !wide_ok(v_last, beta_last, n_cand))
+  if (mode_ok(integrator, true, true) != MPC_OK || !is_cum(integrator) ||
+      !chain_ctl_ok(v_last, beta_last, n_cand, integrator))
     return MPC_ERR_UNSUPPORTED;
   if (ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
-  k_episode_p2p_flush<MPC_INTEG_RECT, kRotCum>
-      <<<1, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
-          *cfg, static_cast<EpisodeState*>(state), mailbox, last_epoch, world,
-          static_cast<const Rec*>(ws_last), static_cast<int>(rollout_grid<kCplWide>(n_cand)),
-          v_last, beta_last, n_cand, n_steps, index_base, out, log, log_capacity);
+  auto launch = [&](auto tiled_tag) {
+    constexpr bool T = decltype(tiled_tag)::value;
+    k_episode_p2p_flush<MPC_INTEG_RECT, kRotCum, T>
+        <<<1, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+            *cfg, static_cast<EpisodeState*>(state), mailbox, last_epoch, world,
+            static_cast<const Rec*>(ws_last), static_cast<int>(rollout_grid<kCplWide>(n_cand)),
+            v_last, beta_last, n_cand, n_steps, index_base, out, log, log_capacity);
+  };
+  if (is_tiled(integrator))
+    launch(std::true_type{});
+  else
+    launch(std::false_type{});
   return last_hip_status();
 }
 

@@ -489,7 +489,23 @@ class DeviceEpisode:
         self.steps_enqueued = 0
         self._pending = None
 
+    @staticmethod
+    def _is_tiled(controls):
+        return isinstance(controls, torch.Tensor)
+
+    def _ptrs(self, controls):
+        """(v pointer, beta pointer, integrator id) of a checked control batch:
+        SoA (v, beta) or a tiled tensor (MPC_LAYOUT_TILED: beta = v + 512)."""
+        from .abi import MPC_LAYOUT_TILED, MPC_TILE
+        if self._is_tiled(controls):
+            p = controls.data_ptr()
+            return p, p + 8 * MPC_TILE, self._integ | MPC_LAYOUT_TILED
+        v, b = controls
+        return v.data_ptr(), b.data_ptr(), self._integ
+
     def _check_controls(self, controls):
+        if self._is_tiled(controls):
+            return self._check_tiled(controls)
         v, b = controls
         key = (id(v), id(b), v.data_ptr(), b.data_ptr())
         if key in self._checked:         # a resident batch seen before: checked once
@@ -504,41 +520,64 @@ class DeviceEpisode:
             self._checked[key] = (v, b)   # holds the tensors: ids stay unique
         return v, b
 
+    def _check_tiled(self, t):
+        from .abi import MPC_TILE
+        key = (id(t), t.data_ptr())
+        if key in self._checked:
+            return t
+        if (tuple(t.shape) != (-(-self.n_local // MPC_TILE), self.n_steps, 2, MPC_TILE)
+                or t.dtype != torch.float64 or not t.is_contiguous()
+                or t.device != self.v_sc.device or t.data_ptr() % 16):
+            raise ValueError("tiled controls must be a contiguous 16-B aligned float64 "
+                             "[ceil(n_local / 512), n_steps, 2, 512] tensor on the episode's "
+                             "device (Expansion.sample_controls_tiled)")
+        if len(self._checked) < 4096:
+            self._checked[key] = t
+        return t
+
     def _chain_step(self, controls, events=None):
         """One chained launch: this step's rollout + the previous step's
         completion (one GPU: finalize + update; multi-GPU: selection over the
         gathered winners + update), then on multi-GPU this step's local
         finalize and the all_gather."""
         L, st = self.lib, self._stream()
-        v, b = self._check_controls(controls)
-        self.cur = (v, b)
+        ctl = self._check_controls(controls)
+        tiled = self._is_tiled(ctl)
+        if tiled and self.exchange and not self.p2p:
+            raise ValueError("tiled controls: the one-GPU and P2P chained steps only")
+        self.cur = ctl
+        vp, bp, integ = self._ptrs(ctl)
         ws, ws_prev = self._ws[0], self._ws[1]
         pend = self._pending
+        pv = pb = None
+        if not self.exchange or self.p2p:   # (the all_gather forms pend the gathered bytes)
+            if pend is not None and self._is_tiled(pend) != tiled:
+                raise ValueError("a chained episode keeps one control layout until its flush")
+            if pend is not None:
+                pv, pb = self._ptrs(pend)[:2]
         if events:
             events[0].record()
         if not self.exchange:
-            pv, pb = (pend[0].data_ptr(), pend[1].data_ptr()) if pend else (None, None)
             native.check(L.mpc_episode_chain_step(
                 ctypes.byref(self.cfg), self.state.data_ptr(), 1, self._next_epoch(),
-                v.data_ptr(), b.data_ptr(),
-                self.n_local, self.n_steps, self.lo, self._integ, ws.data_ptr(),
+                vp, bp,
+                self.n_local, self.n_steps, self.lo, integ, ws.data_ptr(),
                 ws_prev.data_ptr(), ws.numel(), pv, pb, self.local.data_ptr(), None, 0,
                 self.log.data_ptr(), self.log_capacity, st), "mpc_episode_chain_step")
-            self._pending = (v, b)
+            self._pending = ctl
         elif self.p2p:
             # one launch: rollout of step k; its block 0 completes step k-1 —
             # this rank's candidate posted to every mailbox over xGMI, the
             # world's awaited, selection + update (no collective, no host step)
             epoch = self._next_epoch()
-            pv, pb = (pend[0].data_ptr(), pend[1].data_ptr()) if pend else (None, None)
             native.check(L.mpc_episode_p2p_step(
                 ctypes.byref(self.cfg), self.state.data_ptr(), epoch,
-                self._prev_epoch if pend is not None else 0, v.data_ptr(), b.data_ptr(),
-                self.n_local, self.n_steps, self.lo, self._integ, ws.data_ptr(),
+                self._prev_epoch if pend is not None else 0, vp, bp,
+                self.n_local, self.n_steps, self.lo, integ, ws.data_ptr(),
                 ws_prev.data_ptr(), ws.numel(), pv, pb, ctypes.c_void_p(self._mailbox),
                 self.world, self.winner.data_ptr(), self.log.data_ptr(), self.log_capacity, st),
                 "mpc_episode_p2p_step")
-            self._pending = (v, b)
+            self._pending = ctl
             self._prev_epoch = epoch
         elif not self.overlap:
             # one launch (selection of step k-1 over the gathered candidates +
@@ -546,7 +585,7 @@ class DeviceEpisode:
             # all_gather of the 536-B candidates
             native.check(L.mpc_episode_exchange_step(
                 ctypes.byref(self.cfg), self.state.data_ptr(), self._next_epoch(),
-                v.data_ptr(), b.data_ptr(), self.n_local, self.n_steps, self.lo, self._integ,
+                vp, bp, self.n_local, self.n_steps, self.lo, self._integ,
                 ws.data_ptr(), ws.numel(), pend.data_ptr() if pend is not None else None,
                 self.world if pend is not None else 0, self.winner.data_ptr(),
                 self.cand.data_ptr(), self.log.data_ptr(), self.log_capacity, st),
@@ -562,7 +601,7 @@ class DeviceEpisode:
             epoch = self._next_epoch()
             native.check(L.mpc_episode_exchange_step2(
                 ctypes.byref(self.cfg), self.state.data_ptr(), epoch,
-                self._pend_epoch if pend is not None else 0, v.data_ptr(), b.data_ptr(),
+                self._pend_epoch if pend is not None else 0, vp, bp,
                 self.n_local, self.n_steps, self.lo, self._integ, ws.data_ptr(), ws.numel(),
                 self._gathered.data_ptr() if pend is not None else None,
                 self.world if pend is not None else 0, self.winner.data_ptr(),
@@ -599,17 +638,17 @@ class DeviceEpisode:
             return
         L, st = self.lib, self._stream()
         if not self.exchange:
-            v, b = pend
+            vp, bp, integ = self._ptrs(pend)
             native.check(L.mpc_episode_finalize(
-                self.state.data_ptr(), v.data_ptr(), b.data_ptr(), self.n_local, self.n_steps,
-                self.lo, self._integ, self._ws[1].data_ptr(), self._ws[1].numel(),
+                self.state.data_ptr(), vp, bp, self.n_local, self.n_steps,
+                self.lo, integ, self._ws[1].data_ptr(), self._ws[1].numel(),
                 self.local.data_ptr(), ctypes.byref(self.cfg), self.log.data_ptr(),
                 self.log_capacity, st), "mpc_episode_finalize")
         elif self.p2p:
-            v, b = pend
+            vp, bp, integ = self._ptrs(pend)
             native.check(L.mpc_episode_p2p_flush(
-                ctypes.byref(self.cfg), self.state.data_ptr(), self._prev_epoch, v.data_ptr(),
-                b.data_ptr(), self.n_local, self.n_steps, self.lo, self._integ,
+                ctypes.byref(self.cfg), self.state.data_ptr(), self._prev_epoch, vp,
+                bp, self.n_local, self.n_steps, self.lo, integ,
                 self._ws[1].data_ptr(), self._ws[1].numel(), ctypes.c_void_p(self._mailbox),
                 self.world, self.winner.data_ptr(), self.log.data_ptr(), self.log_capacity, st),
                 "mpc_episode_p2p_flush")
@@ -703,6 +742,8 @@ class DeviceEpisode:
         """The streaming rollout/arg-min kernel alone on the current controls
         (writes only the workspace block records; the episode is unchanged)."""
         self.flush()
+        if self._is_tiled(self.cur):
+            raise ValueError("the streaming kernel alone reads SoA controls")
         v, b = self.cur
         native.check(self.lib.mpc_episode_partials(
             self.state.data_ptr(), v.data_ptr(), b.data_ptr(), self.n_local,
@@ -722,13 +763,21 @@ class DeviceEpisode:
         self.steps_enqueued += 1
 
     def step(self, events=None, controls=None):
+        """One MPC step.  controls: this step's resident candidates — SoA
+        (v_sc, beta_sc) [n_steps, n_local] or, for the chained steps (one GPU or
+        P2P), a tiled tensor (Expansion.sample_controls_tiled); None: the
+        device sampler draws them."""
         if self.chain and controls is not None and self._chainable(controls):
             self._chain_step(controls, events)
             return
+        if controls is not None and self._is_tiled(controls):
+            raise ValueError("tiled controls: chained rect+cum steps only (chain=True)")
         self.expand(events, controls)
         self.advance()
 
     def _chainable(self, controls):
+        if self._is_tiled(controls):
+            return self.integrator == "rect+cum" and self.n_local % 2 == 0
         v, b = controls
         return (self.integrator == "rect+cum" and self.n_local % 2 == 0
                 and v.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)

@@ -160,6 +160,42 @@ class Expansion:
         native.check(st, "mpc_sample_controls")
         return v_out, beta_out
 
+    def sample_controls_tiled(self, v_grid, beta_grid, n_cand, n_steps, seed, index_base=0,
+                              const_prefix=True):
+        """The same candidates as sample_controls in the TILED layout
+        (MPC_LAYOUT_TILED): a tensor [tiles, n_steps, 2, MPC_TILE] (v then
+        beta per tile and step); tiled_to_soa() gives the SoA view's values."""
+        from .abi import MPC_TILE
+        tiles = -(-n_cand // MPC_TILE)
+        out = torch.empty((tiles, n_steps, 2, MPC_TILE), dtype=torch.float64, device=self.device)
+        st = self.lib.mpc_sample_controls_tiled(
+            v_grid.data_ptr(), v_grid.numel(), beta_grid.data_ptr(), beta_grid.numel(),
+            n_cand, n_steps, int(seed) & 0xFFFFFFFFFFFFFFFF, int(index_base), int(const_prefix),
+            out.data_ptr(), _stream_ptr())
+        native.check(st, "mpc_sample_controls_tiled")
+        return out
+
+
+def tiled_to_soa(tiles, n_cand):
+    """(v, beta) step-major [n_steps, n_cand] copies of a tiled control tensor
+    [tiles, n_steps, 2, MPC_TILE] (same device)."""
+    t, ns = tiles.shape[0], tiles.shape[1]
+    soa = tiles.permute(2, 1, 0, 3).reshape(2, ns, t * tiles.shape[3])[:, :, :n_cand]
+    return soa[0].contiguous(), soa[1].contiguous()
+
+
+def soa_to_tiled(v, beta):
+    """The tiled tensor [tiles, n_steps, 2, MPC_TILE] of SoA controls (the last
+    tile padded with copies of the last candidate)."""
+    from .abi import MPC_TILE
+    ns, n = v.shape
+    tiles = -(-n // MPC_TILE)
+    pad = tiles * MPC_TILE - n
+    vb = torch.stack([v, beta])                                  # [2, ns, n]
+    if pad:
+        vb = torch.cat([vb, vb[:, :, -1:].expand(2, ns, pad)], dim=2)
+    return vb.reshape(2, ns, tiles, MPC_TILE).permute(2, 1, 0, 3).contiguous()
+
 
 def fulltree_argmin(engine, problem, v_grid, beta_grid, incumbent, integrator="qk21", shard=0,
                     n_shards=1):

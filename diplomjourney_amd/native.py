@@ -47,7 +47,7 @@ EXPORTS = (
     "mpc_ipc_open", "mpc_ipc_close", "mpc_peer_enable", "mpc_episode_p2p_step",
     "mpc_episode_p2p_flush",
     "mpc_fulltree_episodes_state_bytes", "mpc_fulltree_episodes_reset",
-    "mpc_fulltree_episodes_run",
+    "mpc_fulltree_episodes_run", "mpc_stream_probe_tiled", "mpc_sample_controls_tiled",
 )
 
 HIPCC_FLAGS = [
@@ -135,6 +135,12 @@ def lib():
                                              ctypes.c_size_t, _P, _P]
     L.mpc_stream_probe.restype = ctypes.c_int
     L.mpc_stream_probe.argtypes = [_P, _P, _I64, _I32, _P, ctypes.c_size_t, _P]
+    if not (_LIB_OVERRIDE and not hasattr(L, "mpc_stream_probe_tiled")):
+        L.mpc_stream_probe_tiled.restype = ctypes.c_int
+        L.mpc_stream_probe_tiled.argtypes = [_P, _I64, _I32, _P, ctypes.c_size_t, _P]
+        L.mpc_sample_controls_tiled.restype = ctypes.c_int
+        L.mpc_sample_controls_tiled.argtypes = [_P, _I32, _P, _I32, _I64, _I32, ctypes.c_uint64,
+                                                _I64, _I32, _P, _P]
     L.mpc_rcp_estimate.restype = ctypes.c_int
     L.mpc_rcp_estimate.argtypes = [_P, _P, _I64, _P]
     L.mpc_select_winner.restype = ctypes.c_int

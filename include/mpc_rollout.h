@@ -71,6 +71,21 @@ enum { MPC_INTEG_QK21 = 0, MPC_INTEG_RECT = 1 };
  * episode step (mpc_episode_chain_step) roll out step k while step k-1 is
  * still being selected.  Irregular candidates as above. */
 #define MPC_HEADING_CUMULATIVE 0x200
+/* Control layout flag, OR'ed into `integrator` of the chained one-GPU and P2P
+ * episode entries and their flush (mpc_episode_chain_step,
+ * mpc_episode_finalize, mpc_episode_p2p_step, mpc_episode_p2p_flush): the
+ * candidates are TILED instead of step-major SoA — tile t of 512 consecutive
+ * candidates holds, for each step s, its 512 v values then its 512 beta values,
+ *   v    (c, s) = base[(c / 512) * 1024 * n_steps + s * 1024 + c % 512]
+ *   beta (c, s) = the same + 512
+ * (mpc_tiled_index; allocation: ceil(n_cand / 512) * 1024 * n_steps doubles).
+ * The caller passes v_sc = base and beta_sc = base + 512.  One tile's whole
+ * horizon is one contiguous 8-KiB-per-step run, so a tile block's control
+ * stream stays within a few DRAM pages instead of striding by 8 * n_cand
+ * bytes per step (measured, tools/micro/layout_probe.hip: 6.31 vs 6.14 TB/s at
+ * 1e6 x N = 10).  mpc_sample_controls_tiled writes this layout. */
+#define MPC_LAYOUT_TILED 0x400
+#define MPC_TILE 512
 
 /* One MPC problem (one robot at one MPC step). */
 typedef struct mpc_problem {
@@ -166,6 +181,10 @@ int mpc_select_winner(const mpc_result_t* results, int32_t n, double incumbent,
  * written). */
 int mpc_stream_probe(const double* v_sc, const double* beta_sc, int64_t n_cand,
                      int32_t n_steps, void* sink, size_t sink_bytes, mpc_stream_t stream);
+/* The same probe over TILED controls (MPC_LAYOUT_TILED; tiles = the tiled
+ * buffer's base): the ceiling of the chained kernel's tiled access pattern. */
+int mpc_stream_probe_tiled(const double* tiles, int64_t n_cand, int32_t n_steps, void* sink,
+                           size_t sink_bytes, mpc_stream_t stream);
 
 /* Verification probe (not a reference operation): the hardware reciprocal
  * estimate the rollout's steering tangent starts from (v_rcp_f64, before its
@@ -187,6 +206,20 @@ int mpc_sample_controls(const double* v_grid, int32_t n_v, const double* beta_gr
                         int32_t n_beta, int64_t n_cand, int32_t n_steps, uint64_t seed,
                         int64_t index_base, int32_t const_prefix, double* v_sc,
                         double* beta_sc, int64_t ld, mpc_stream_t stream);
+/* The same candidates written in the TILED layout (MPC_LAYOUT_TILED) into
+ * tiles[ceil(n_cand / 512) * 1024 * n_steps] (16-B aligned, n_cand even); the
+ * last tile's padding slots hold the generator's values of the global indices
+ * that follow (they are never read as candidates). */
+int mpc_sample_controls_tiled(const double* v_grid, int32_t n_v, const double* beta_grid,
+                              int32_t n_beta, int64_t n_cand, int32_t n_steps, uint64_t seed,
+                              int64_t index_base, int32_t const_prefix, double* tiles,
+                              mpc_stream_t stream);
+/* Offset (in doubles, from the tiled buffer's base) of candidate c's v at step
+ * s; its beta is 512 further. */
+static inline int64_t mpc_tiled_index(int64_t c, int32_t s, int32_t n_steps) {
+  return (c / MPC_TILE) * 2 * MPC_TILE * (int64_t)n_steps + (int64_t)s * 2 * MPC_TILE +
+         c % MPC_TILE;
+}
 
 
 /* ---------------------------------------------------------------------------

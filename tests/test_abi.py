@@ -14,9 +14,12 @@ HEADER = native.HEADER
 
 
 def _declared():
+    """The functions the header declares for the library to export (its static
+    inline helpers, defined in the header itself, excluded)."""
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return set(re.findall(r"\b(mpc_[a-z_0-9]+)\s*\(", text))
+    inline = set(re.findall(r"static\s+inline\s+[a-z_0-9]+\s+(mpc_[a-z_0-9]+)\s*\(", text))
+    return set(re.findall(r"\b(mpc_[a-z_0-9]+)\s*\(", text)) - inline
 
 
 @pytest.fixture(scope="module")
@@ -201,3 +204,70 @@ def test_p2p_exchange_argument_validation_without_gpu():
     assert flush(world=0) == abi.MPC_ERR_ARG
     assert flush(out=None) == abi.MPC_ERR_ARG
     assert flush(ws=None) == abi.MPC_ERR_ARG
+
+
+def test_tiled_layout_argument_validation_without_gpu():
+    """MPC_LAYOUT_TILED: accepted only by the chained one-GPU / P2P entries and
+    their flush; the tiled buffer's beta must be its base + 512, n_cand even.
+    Every rejection happens before any HIP call."""
+    from diplomjourney_amd.episode import reference_episode_config
+    L = native.lib()
+    cfg = reference_episode_config()
+    t = abi.MPC_LAYOUT_TILED
+    cum = abi.INTEGRATORS["rect+cum"]
+    base = ctypes.c_void_p(0x10000)
+    b_ok = ctypes.c_void_p(0x10000 + 8 * abi.MPC_TILE)
+    b_bad = ctypes.c_void_p(0x20000)
+    f = ctypes.c_void_p(0x1000)
+
+    def chain(integ=cum | t, v=base, b=b_ok, n=1024):
+        return L.mpc_episode_chain_step(ctypes.byref(cfg), f, 1, 1, v, b, n, 10, 0, integ, f, f,
+                                        1 << 24, None, None, f, None, 0, f, 8, None)
+    assert chain(b=b_bad) == abi.MPC_ERR_UNSUPPORTED          # beta != base + 512
+    assert chain(n=1023) == abi.MPC_ERR_UNSUPPORTED           # two candidates per lane
+    assert chain(v=ctypes.c_void_p(0x10008), b=ctypes.c_void_p(0x10008 + 4096)) == \
+        abi.MPC_ERR_UNSUPPORTED                               # 16-B aligned base
+    assert chain(integ=abi.INTEGRATORS["rect"] | t) == abi.MPC_ERR_UNSUPPORTED   # chained: +cum
+    # entries that read SoA controls refuse the flag
+    assert L.mpc_episode_partials(f, base, b_ok, 1024, 10, cum | t, f, 1 << 24, None) == \
+        abi.MPC_ERR_UNSUPPORTED
+    assert L.mpc_episode_exchange_step(ctypes.byref(cfg), f, 1, base, b_ok, 1024, 10, 0, cum | t,
+                                       f, 1 << 24, None, 0, f, f, f, 8, None) == \
+        abi.MPC_ERR_UNSUPPORTED
+    # the flush of a tiled chained step needs the episode update (advance)
+    assert L.mpc_episode_finalize(f, base, b_ok, 1024, 10, 0, cum | t, f, 1 << 24, f, None, f,
+                                  8, None) == abi.MPC_ERR_UNSUPPORTED
+    sink = ctypes.c_void_p(0x40000)
+    assert L.mpc_stream_probe_tiled(ctypes.c_void_p(0x10008), 1024, 10, sink, 1 << 30, None) == \
+        abi.MPC_ERR_UNSUPPORTED
+    assert L.mpc_stream_probe_tiled(base, 1024, 0, sink, 1 << 30, None) == abi.MPC_ERR_ARG
+    assert L.mpc_sample_controls_tiled(f, 3, f, 4, 1023, 10, 1, 0, 1, base, None) == \
+        abi.MPC_ERR_ARG
+
+
+def test_tiled_index_header_matches_python(tmp_path):
+    """The header's mpc_tiled_index (C) == soa_to_tiled / tiled_to_soa
+    (torch, CPU): every candidate and step of a ragged last tile."""
+    import torch
+    from diplomjourney_amd.expansion import soa_to_tiled, tiled_to_soa
+    n, ns = 1300, 3
+    src = tmp_path / "ti.c"
+    src.write_text(
+        '#include <stdio.h>\n#include "mpc_rollout.h"\n'
+        "int main(void) { for (int s = 0; s < %d; ++s) for (long c = 0; c < %d; ++c)"
+        ' printf("%%ld\\n", (long)mpc_tiled_index(c, s, %d)); return 0; }\n' % (ns, n, ns))
+    exe = tmp_path / "ti"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), "-o", str(exe), str(src)],
+                   check=True)
+    idx = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    v = torch.arange(ns * n, dtype=torch.float64).reshape(ns, n)
+    b = -v - 1
+    t = soa_to_tiled(v, b)
+    flat = t.reshape(-1)
+    for s in range(ns):
+        for c in range(0, n, 7):
+            o = idx[s * n + c]
+            assert flat[o] == v[s, c] and flat[o + abi.MPC_TILE] == b[s, c]
+    v2, b2 = tiled_to_soa(t, n)
+    assert torch.equal(v2, v) and torch.equal(b2, b)

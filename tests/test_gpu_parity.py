@@ -1112,6 +1112,85 @@ def test_p2p_exchange_one_rank_eager_and_graph(engine, wheelbase, n, cap):
         ep.close()
 
 
+@pytest.mark.parametrize("wheelbase,n,ns", [(0.5, 100_000, 3), (0.45, 60_000, 10),
+                                            (0.5, 1_000_000, 10), (0.5, 1_250_000, 12)])
+def test_tiled_chained_episode_matches_soa(engine, wheelbase, n, ns):
+    """MPC_LAYOUT_TILED (the bench's resident layout): the tiled sampler's
+    candidates are the SoA sampler's, and the chained episode over tiled
+    batches logs exactly the chained episode over the same SoA batches —
+    70 steps with max_steps = 40 (a restart inside), both wheelbase forms, a
+    ragged last tile (n % 512 != 0), config C's and D's sizes — with the same
+    final result record."""
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.episode import DeviceEpisode
+    from diplomjourney_amd.expansion import tiled_to_soa
+    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
+    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
+    soa = [engine.sample_controls(V, B, n, ns, 900 + i) for i in range(4)]
+    til = [engine.sample_controls_tiled(V, B, n, ns, 900 + i) for i in range(4)]
+    for (v, b), t in zip(soa, til):
+        v2, b2 = tiled_to_soa(t, n)
+        assert torch.equal(v, v2) and torch.equal(b, b2)
+    eps = [DeviceEpisode(engine, n, ns, integrator="rect+cum", chain=True, log_capacity=128,
+                         max_steps=40, L=wheelbase) for _ in range(2)]
+    for i in range(70):
+        eps[0].step(controls=soa[i % 4])
+        eps[1].step(controls=til[i % 4])
+    logs = [_episode_log(e) for e in eps]
+    assert logs[0] == logs[1] and len(logs[0]) == 70
+    assert len({r[9] for r in logs[0]}) >= 2                     # a restart inside
+    assert torch.equal(eps[0].local, eps[1].local)
+    assert eps[1].chain_error() == 0
+
+
+def test_tiled_p2p_one_rank_and_probe(engine):
+    """Tiled controls through the P2P exchange form (one rank: eager steps,
+    then a captured sequence of odd length replayed three times) log the
+    single-GPU SoA episode; the tiled stream probe runs on the same batches."""
+    import ctypes
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.episode import DeviceEpisode
+    from diplomjourney_amd.expansion import tiled_to_soa
+    n, ns, steps, cap, reps = 300_000, 10, 12, 5, 3
+    V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
+    B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
+    til = [engine.sample_controls_tiled(V, B, n, ns, 2900 + i) for i in range(steps)]
+    soa = [tiled_to_soa(t, n) for t in til]
+    half = steps - cap
+    ref = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64)
+    for i in list(range(steps)) + list(range(half, steps)) * (reps - 1):
+        ref.step(controls=soa[i])
+    want = _episode_log(ref)
+    ep = DeviceEpisode(engine, n, ns, integrator="rect+cum", log_capacity=64, exchange=True,
+                       chain=True, p2p=True)
+    try:
+        for i in range(half):
+            ep.step(controls=til[i])
+        ep.flush()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        n0 = ep.steps_enqueued
+        with torch.cuda.graph(g):
+            for i in range(half, steps):
+                ep.step(controls=til[i])
+            ep.flush()
+        ep.steps_enqueued = n0
+        for _ in range(reps):
+            g.replay()
+            ep.steps_enqueued += steps - half
+        torch.cuda.synchronize()
+        assert _episode_log(ep) == want
+        assert ep.chain_error() == 0
+    finally:
+        ep.close()
+    sink = torch.empty(2048 * 256, dtype=torch.int64, device="cuda")
+    from diplomjourney_amd import native
+    native.check(native.lib().mpc_stream_probe_tiled(
+        til[0].data_ptr(), n, ns, sink.data_ptr(), sink.numel() * 8,
+        ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "mpc_stream_probe_tiled")
+    torch.cuda.synchronize()
+
+
 def test_p2p_exchange_two_ranks_on_one_gpu(engine, tmp_path):
     """The collective-free exchange with 2 ranks (two processes sharing this
     GPU; the mailboxes' IPC handles exchanged once over gloo, every step's

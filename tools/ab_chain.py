@@ -23,6 +23,18 @@ def child():
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
     pool = [eng.sample_controls(V, B, n, ns, 0x5EED0000 + i) for i in range(8)]
+    if os.environ.get("AB_PAD"):
+        # v and beta of a batch in ONE allocation with a tile of padding after
+        # them, so a variant reading tile-contiguous blocks stays in bounds
+        padded = []
+        for v, b in pool:
+            buf = torch.empty(2 * ns * n + ns * 1024, dtype=torch.float64, device="cuda")
+            buf[:ns * n].copy_(v.reshape(-1))
+            buf[ns * n:2 * ns * n].copy_(b.reshape(-1))
+            buf[2 * ns * n:].fill_(0.25)
+            padded.append((buf[:ns * n].view(ns, n), buf[ns * n:2 * ns * n].view(ns, n), buf))
+        pool = [(v, b) for v, b, _ in padded]
+        keep = padded   # noqa: F841 (holds the buffers)
     ep = DeviceEpisode(eng, n, ns, integrator="rect+cum", chain=True, log_capacity=8192)
     out = {}
     for name, fn in (("chain", lambda i: ep.step(controls=pool[i % 8])),

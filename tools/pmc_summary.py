@@ -1,7 +1,7 @@
 """Summarise tools/pmc.sh counter passes for the rollout kernel into a JSON
 file bench.py reads for roofline.traffic (--traffic-json).
 
-    python tools/pmc_summary.py gpurun_out/<tag> out.json [algorithmic_bytes] [kernel] [label]
+    python tools/pmc_summary.py gpurun_out/<tag> out.json [algorithmic_bytes] [kernel] [label] [layout]
 
 kernel: a substring of the rocprof kernel name (e.g. "k_episode_chain<1, 2, 3"
 for the exchange form); label: the name written to the summary's "kernel"
@@ -23,6 +23,7 @@ def main():
     algo = float(sys.argv[3]) if len(sys.argv) > 3 else 160e6   # 16 B x N x C of the runs
     kernel = sys.argv[4] if len(sys.argv) > 4 else "k_rollout_argmin_stream"
     label = sys.argv[5] if len(sys.argv) > 5 else kernel
+    layout = sys.argv[6] if len(sys.argv) > 6 else "soa"   # the controls' layout of the runs
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     for f in sorted(glob.glob(os.path.join(root, "pmc*", "p_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
@@ -43,6 +44,7 @@ def main():
                       + med.get("SQ_INSTS_VALU_MUL_F64", 0) + med.get("SQ_INSTS_VALU_TRANS_F64", 0))
     res = {
         "kernel": label,
+        "layout": layout,
         "kernel_name_filter": kernel,
         "fp64_ops_per_launch": f64,
         "hbm_bytes_per_launch": 2.0 * fetch_b + write_b,

@@ -8,7 +8,8 @@ the bench default's launch: rollout of step k + completion of step k-1);
 "xchg": the exchange form of the chained step (mpc_episode_exchange_step +
 the RCCL all_gather, over a 1-rank nccl group: the N > 1 bench's launch);
 "p2p": the collective-free exchange form (mpc_episode_p2p_step, one rank: the
-N > 1 bench's launch);
+N > 1 bench's launch); chain / p2p with MPC_LAYOUT=tiled in the environment:
+tiled batches (MPC_LAYOUT_TILED, the bench's default);
 "generated": generated-controls episode steps (k_rollout_generated, rect+cum);
 "fulltree": config F's full-tree MPC steps (k_ft_leaves, S1 = 451, n_cand and
 n_steps ignored);
@@ -75,6 +76,9 @@ def main():
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
     pool = [eng.sample_controls(V, B, n, ns, 7 + i) for i in range(nb)]
+    if integ in ("chain", "p2p") and os.environ.get("MPC_LAYOUT") == "tiled":
+        # the bench's resident layout of the chained steps (MPC_LAYOUT_TILED)
+        pool = [eng.sample_controls_tiled(V, B, n, ns, 7 + i) for i in range(nb)]
     if integ in ("chain", "xchg", "p2p"):
         from diplomjourney_amd.episode import DeviceEpisode
         xchg = integ == "xchg"
