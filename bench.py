@@ -35,9 +35,10 @@ input mode.  --host-loop runs the host-driven episode instead.
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the
 chained k_episode_chain by default, k_rollout_argmin_stream for two-launch
 steps): algorithmic bytes 16 B per candidate-step (fp64 v and beta read once)
-/ its average duration, from HIP events around 100 back-to-back launches on
-the episode's stream and controls; with chained steps `roofline_rollout_only`
-adds the same controls through the rollout kernel alone.
+/ its average duration, from HIP events around a graph replay of 200
+back-to-back launches on the episode's stream and controls (graph_timed);
+with chained steps `roofline_rollout_only` adds the same controls through the
+rollout kernel alone.
 `cpu_baseline` is the reference-structured Python port (scipy quad) on this
 host's cores, rank 0 at N=1 only, on a bounded sample of the same candidates;
 it runs before the GPU is initialised (it forks worker processes).
@@ -801,13 +802,12 @@ def finish(ep, have_group):
         dist.destroy_process_group()
 
 
-def stream_ceiling(ep, pool, reps=100, warm=100):
+def stream_ceiling(ep, pool, reps=200, warm=100):
     """Measured read ceiling of the rollout's own access pattern on this GPU:
     mpc_stream_probe (the streaming kernel's grid, tiles and LDS-DMA control
     ring, no arithmetic; mpc_stream_probe_tiled for tiled batches) over the
-    same resident batches, REPS back-to-back
-    launches between HIP events on the episode's stream, rotating over the
-    pool as kernel_pass does.  Returns (GB/s of the 16 B per candidate-step
+    same resident batches, REPS back-to-back launches replayed from a HIP
+    graph (graph_timed), rotating over the pool as kernel_pass does.  Returns (GB/s of the 16 B per candidate-step
     read, ms per launch)."""
     import ctypes
     import torch
@@ -827,15 +827,7 @@ def stream_ceiling(ep, pool, reps=100, warm=100):
                                       sink.numel() * 8, st)
         if rc != 0:
             raise RuntimeError(f"mpc_stream_probe: status {rc}")
-    for i in range(warm):
-        one(i)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for i in range(reps):
-        one(i + 1)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+    ms, _ = graph_timed(one, reps, warm)
     return 16.0 * ns * n / (ms * 1e-3) / 1e9, ms
 
 
@@ -1021,28 +1013,70 @@ def run_steps(args, ep, pool, use_graph, world, device):
             "kernel_in_step_ms": sum(a.elapsed_time(b) for a, b in kern) / len(kern)}
 
 
-def kernel_pass(ep, pool, reps=100, warm=200):
-    """The rollout kernel alone: REPS back-to-back launches between two HIP
-    events on the launch stream, rotating over the resident batches (at least
-    4 x the batch bytes between two uses of a batch, so no launch is served
-    from the 256 MiB Infinity Cache; events around the single launch inside a
-    step would add their own packet overhead), after WARM untimed ones (see
-    chain_pass)."""
+def graph_timed(launch, reps, warm, tail=None, on_capture_fail=None, align=None):
+    """Device time per launch of `launch(i)`: WARM eager launches, then REPS
+    launches (+ `tail()`, e.g. the flush that ends a captured chained
+    sequence) captured into one HIP graph, replayed once untimed and once
+    between two HIP events on the current stream.  The replay runs the
+    launches back to back on the GPU with no host enqueue in between — eagerly
+    launched steps (~30 us of Python + ctypes each) are host-bound on a slow
+    host core and would time the host instead (measured: 31.6 vs 29.7 us per
+    chained launch on one box).  Falls back to timed eager launches if capture
+    is refused.  align(): called right before the timed replay (multi-rank:
+    a barrier, so no rank's timed replay waits for a peer still in its
+    untimed one).  Returns (ms per launch, "graph" | "eager")."""
     import torch
-    k0 = torch.cuda.Event(enable_timing=True)
-    k1 = torch.cuda.Event(enable_timing=True)
+    for i in range(warm):
+        launch(i)
+    if tail:
+        tail()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    try:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for i in range(reps):
+                launch(i + 1)
+            if tail:
+                tail()
+    except Exception:   # capture refused: time eager launches
+        if on_capture_fail:
+            on_capture_fail()
+        torch.cuda.synchronize()
+        if align:
+            align()
+        e0.record()
+        for i in range(reps):
+            launch(i + 1)
+        e1.record()
+        if tail:
+            tail()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps, "eager"
+    g.replay()
+    torch.cuda.synchronize()
+    if align:
+        align()
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps, "graph"
+
+
+def kernel_pass(ep, pool, reps=200, warm=200):
+    """The rollout kernel alone: REPS back-to-back launches replayed from a
+    HIP graph (graph_timed), rotating over the resident batches (at least 4 x
+    the batch bytes between two uses of a batch, so no launch is served from
+    the 256 MiB Infinity Cache)."""
     saved = ep.cur
-    for i in range(warm + 1):
+
+    def one(i):
         ep.cur = pool[i % len(pool)]
         ep.partials()
-    k0.record()
-    for i in range(reps):
-        ep.cur = pool[(i + 1) % len(pool)]
-        ep.partials()
-    k1.record()
-    torch.cuda.synchronize()
+    ms, _ = graph_timed(one, reps, warm)
     ep.cur = saved
-    return k0.elapsed_time(k1) / reps
+    return ms
 
 
 def max_over_ranks(x, device):
@@ -1154,25 +1188,26 @@ def valu_roofline(kernel, integrator, ms, n_cand, n_steps, note=None):
     return out
 
 
-def chain_pass(ep, pool, reps=100, warm=200):
+def chain_pass(ep, pool, reps=200, warm=200):
     """The chained launch (rollout of step k + completion of step k-1): REPS
-    back-to-back launches between two HIP events on the launch stream,
-    rotating over the resident batches as kernel_pass does, after WARM
-    untimed ones (a short bench run, e.g. --steps 20, leaves the GPU's clocks
-    still ramping: 38 -> 34 us per launch over the first ~400); the episode
-    goes on (the launches are real steps)."""
-    import torch
-    k0 = torch.cuda.Event(enable_timing=True)
-    k1 = torch.cuda.Event(enable_timing=True)
-    for i in range(warm + 1):
+    real steps rotating over the resident batches, captured with the flush
+    that ends the sequence and replayed back to back from a HIP graph
+    (graph_timed; the one flush launch is included, +~0.05 us per launch),
+    after WARM eager ones (the GPU's clocks ramp over the first few hundred
+    launches); the episode goes on."""
+    def one(i):
         ep.step(controls=pool[i % len(pool)])
-    k0.record()
-    for i in range(reps):
-        ep.step(controls=pool[(i + 1) % len(pool)])
-    k1.record()
-    ep.flush()
-    torch.cuda.synchronize()
-    return k0.elapsed_time(k1) / reps
+
+    def lost():                 # a refused capture: the captured steps never ran
+        if hasattr(ep, "_pending"):
+            ep._pending = None
+    import torch.distributed as dist
+    align = dist.barrier if dist.is_initialized() and dist.get_world_size() > 1 else None
+    n0 = ep.steps_enqueued
+    ms, how = graph_timed(one, reps, warm, tail=ep.flush, on_capture_fail=lost, align=align)
+    # warm + 2 replays (or the eager fallback's reps) of real steps ran
+    ep.steps_enqueued = n0 + warm + (2 * reps if how == "graph" else reps)
+    return ms
 
 
 def roofline(achieved, bytes_launch, traffic_json, kernel="k_rollout_argmin_stream",
