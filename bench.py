@@ -555,16 +555,24 @@ def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
     main_run = run_steps(args, ep, pool, use_graph, world, device)
     use_graph = main_run["graph"]
     kern_ms = main_run["kernel_in_step_ms"]
-    if chained:
+    sustained_ms = None
+    if (chained or (xchg_chain and p2p)) and use_graph:
+        # one launch per step, the K of the timed region back to back: HIP
+        # events around them inside the timed replay
+        kern_ms = main_run["kernel_timed_ms"]
+        # the same launches sustained over a longer run (200 eager + 2 x 200
+        # replayed; reported beside the timed region's value)
+        sustained_ms = None if sub else chain_pass(ep, pool)
+    elif chained or (xchg_chain and p2p):
         kern_ms = chain_pass(ep, pool)
+    elif xchg_chain:
+        # the all_gather form has its collective between two launches: a pair
+        # of events per launch
+        kern_ms = exchange_chain_pass(ep, pool)
+    if chained and not sub:
         # for comparison: the same controls through the rollout kernel alone
         # (the chained launch adds block 0's completion of the previous step)
-        rollout_ms = None if sub else kernel_pass(ep, soa_pool(ep, pool))
-    elif xchg_chain:
-        # P2P: no collective between launches, so back-to-back launches
-        # between one pair of events (chain_pass); the all_gather form has its
-        # collective between two launches: a pair of events per launch
-        kern_ms = chain_pass(ep, pool) if p2p else exchange_chain_pass(ep, pool)
+        rollout_ms = kernel_pass(ep, soa_pool(ep, pool))
     elif inputs == "generated":
         pass   # events around the generated rollout + selection (no HBM roofline)
     elif hasattr(ep, "partials"):
@@ -678,6 +686,11 @@ def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
                          else "all_gather (gloo)")),
         "chain_error": chain_err,
         "kernel_ms": kern_ms, "kernel_in_step_ms": main_run["kernel_in_step_ms"],
+        "kernel_ms_note": ("device time per step launch inside the timed region (HIP events "
+                           "around the timed graph replay of the K launches, the closing flush "
+                           "outside)" if (chained or (xchg_chain and p2p)) and use_graph
+                           else "events around back-to-back launches (graph_timed / per launch)"),
+        "kernel_ms_sustained": sustained_ms,
         "roofline": (None if inputs == "generated" else
                      roofline(achieved, bytes_launch, args.traffic_json, kernel=kernel,
                               layout="tiled" if tiled else "soa")),
@@ -814,9 +827,10 @@ def stream_ceiling(ep, pool, reps=200, warm=100):
     lib = ep.lib
     n, ns = ep.n_local, ep.n_steps
     sink = torch.empty(2048 * 256, dtype=torch.int64, device=pool[0][0].device)
-    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     def one(i):
+        # (the current stream at each launch: graph_timed captures on its own)
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         p = pool[i % len(pool)]
         if isinstance(p, torch.Tensor):      # tiled: the chained kernel's tiled pattern
             rc = lib.mpc_stream_probe_tiled(p.data_ptr(), n, ns, sink.data_ptr(),
@@ -924,7 +938,20 @@ LAYOUT_DOC = {
 
 
 def run_steps(args, ep, pool, use_graph, world, device):
-    """Warmup, an eager latency pass (events), then the timed K steps."""
+    """Warmup, the timed K steps, then the eager latency passes.
+
+    With a graph (the default): the K steps are captured once into graph A
+    (and a chained episode's closing flush into graph B, so A holds exactly
+    the K step launches); A + B are replayed untimed until ~300 steps have run
+    (the GPU's clocks ramp over the first few hundred launches: 38 -> 34 us
+    per chained step), then ONE timed replay of A + B between barrier + sync
+    on both sides (host clock: `elapsed`, the value's denominator) with HIP
+    events around A alone on the launch stream: `kernel_timed_ms`, the device
+    time per step launch inside the timed region (for chained steps: the
+    chained kernel's duration, back to back, the roofline's denominator).
+    Then, eagerly: K steps with one event per step start (p50 / p90 of the
+    GPU time per step) and up to 20 steps with events around the step's
+    launch (`kernel_in_step_ms`)."""
     import torch
     import torch.distributed as dist
     from diplomjourney_amd.episode import percentile
@@ -936,15 +963,75 @@ def run_steps(args, ep, pool, use_graph, world, device):
             ep.step(events=events, controls=pool[i % len(pool)])
 
     flush = getattr(ep, "flush", lambda: None)   # completes a chained step left pending
+    Ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     for i in range(args.warmup):
         step(i)
-    # (untimed) until ~10 ms of steps have run: the GPU's clocks ramp over the
-    # first few hundred launches (38 -> 34 us per chained step), which a short
-    # --warmup leaves in the latency pass's p50
-    for i in range(max(0, 300 - args.warmup)):
-        step(i)
     flush()
-    Ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    torch.cuda.synchronize()
+    gA = gB = None
+    if use_graph:
+        n0 = ep.steps_enqueued
+        try:
+            gA = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gA):
+                for i in range(args.steps):
+                    step(i)
+            if getattr(ep, "_pending", None) is not None:
+                gB = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gB):
+                    flush()                  # the K-th step completes in graph B
+        except Exception as e:   # capture refused (e.g. by the collective): launch eagerly
+            print(f"bench: graph capture failed ({type(e).__name__}: {e}); eager launches",
+                  file=sys.stderr, flush=True)
+            gA = gB = None
+            if hasattr(ep, "_pending"):
+                ep._pending = None           # the captured launches never ran
+            torch.cuda.synchronize()
+        ep.steps_enqueued = n0               # captured, not run
+
+    def replay():
+        gA.replay()
+        if gB is not None:
+            gB.replay()
+        ep.steps_enqueued += args.steps
+
+    # untimed: the clock ramp (graph replays, or eager steps)
+    ran = 0
+    while ran < 300:
+        if gA is not None:
+            replay()
+        else:
+            for i in range(args.steps):
+                step(i)
+            flush()
+        ran += args.steps
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = Ev(), Ev()
+    t0 = time.perf_counter()
+    e0.record()
+    if gA is not None:
+        gA.replay()
+        e1.record()
+        if gB is not None:
+            gB.replay()
+        ep.steps_enqueued += args.steps
+    else:
+        for i in range(args.steps):
+            step(i)
+        e1.record()
+        flush()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_timed_ms = e0.elapsed_time(e1) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
     # latency pass: one event per step start (more events per step would add
     # their own host cost to an eagerly launched step)
     marks = [Ev() for _ in range(args.steps + 1)]
@@ -956,58 +1043,15 @@ def run_steps(args, ep, pool, use_graph, world, device):
     flush()
     torch.cuda.synchronize()
     step_gpu_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)]
-    # the rollout launch inside eager steps, events around it
-    n_kern = min(args.steps, 100)
+    # the step's launch inside eager steps, events around it
+    n_kern = min(args.steps, 20)
     kern = [(Ev(), Ev()) for _ in range(n_kern)]
     for i in range(n_kern):
         step(i, kern[i])
     flush()
     torch.cuda.synchronize()
-    # Throughput pass: the K steps captured once into a HIP graph (the episode
-    # lives in HBM, so a replay simply continues it) and replayed: no host
-    # cost between the step's kernels.  Multi-GPU runs capture the RCCL
-    # all_gather into the same graph (nccl backend; gloo runs launch eagerly).
-    graph = None
-    if use_graph:
-        n0 = ep.steps_enqueued
-        try:
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                for i in range(args.steps):
-                    step(i)
-                flush()                      # the K-th step completes inside the graph
-        except Exception as e:   # capture refused (e.g. by the collective): launch eagerly
-            print(f"bench: graph capture failed ({type(e).__name__}: {e}); eager launches",
-                  file=sys.stderr, flush=True)
-            graph = None
-            if hasattr(ep, "_pending"):
-                ep._pending = None           # the captured launches never ran
-            torch.cuda.synchronize()
-        ep.steps_enqueued = n0               # captured, not run
-        if graph is not None:
-            graph.replay()                   # untimed: first replay
-            ep.steps_enqueued += args.steps
-        torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    if graph is not None:
-        graph.replay()
-        ep.steps_enqueued += args.steps
-    else:
-        for i in range(args.steps):
-            step(i)
-        flush()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    return {"elapsed": elapsed, "graph": graph is not None,
+    return {"elapsed": elapsed, "graph": gA is not None,
+            "kernel_timed_ms": kernel_timed_ms,
             "p50_ms": percentile(step_gpu_ms, 50),
             "p90_ms": percentile(step_gpu_ms, 90),
             "kernel_in_step_ms": sum(a.elapsed_time(b) for a, b in kern) / len(kern)}
