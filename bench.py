@@ -569,15 +569,15 @@ def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
         # the all_gather form has its collective between two launches: a pair
         # of events per launch
         kern_ms = exchange_chain_pass(ep, pool)
-    if chained and not sub:
-        # for comparison: the same controls through the rollout kernel alone
-        # (the chained launch adds block 0's completion of the previous step)
-        rollout_ms = kernel_pass(ep, soa_pool(ep, pool))
     elif inputs == "generated":
         pass   # events around the generated rollout + selection (no HBM roofline)
     elif hasattr(ep, "partials"):
         kern_ms = kernel_pass(ep, pool if pool is not None else
                               make_pool(eng, ep, n_steps, 4))
+    if chained and not sub:
+        # for comparison: the same controls through the rollout kernel alone
+        # (the chained launch adds block 0's completion of the previous step)
+        rollout_ms = kernel_pass(ep, soa_pool(ep, pool))
     other = generated = None
     if not args.host_loop and not args.no_second_pass and not sub:
         # the other input mode, same episode machinery, for comparison
