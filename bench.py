@@ -687,8 +687,9 @@ def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
         "chain_error": chain_err,
         "kernel_ms": kern_ms, "kernel_in_step_ms": main_run["kernel_in_step_ms"],
         "kernel_ms_note": ("device time per step launch inside the timed region (HIP events "
-                           "around the timed graph replay of the K launches, the closing flush "
-                           "outside)" if (chained or (xchg_chain and p2p)) and use_graph
+                           "around the timed graph replay, minus the closing flush's own "
+                           "duration %.4f ms, over K)" % main_run["flush_ms"]
+                           if (chained or (xchg_chain and p2p)) and use_graph
                            else "events around back-to-back launches (graph_timed / per launch)"),
         "kernel_ms_sustained": sustained_ms,
         "roofline": (None if inputs == "generated" else
@@ -940,18 +941,19 @@ LAYOUT_DOC = {
 def run_steps(args, ep, pool, use_graph, world, device):
     """Warmup, the timed K steps, then the eager latency passes.
 
-    With a graph (the default): the K steps are captured once into graph A
-    (and a chained episode's closing flush into graph B, so A holds exactly
-    the K step launches); A + B are replayed untimed until ~300 steps have run
-    (the GPU's clocks ramp over the first few hundred launches: 38 -> 34 us
-    per chained step), then ONE timed replay of A + B between barrier + sync
-    on both sides (host clock: `elapsed`, the value's denominator) with HIP
-    events around A alone on the launch stream: `kernel_timed_ms`, the device
-    time per step launch inside the timed region (for chained steps: the
-    chained kernel's duration, back to back, the roofline's denominator).
-    Then, eagerly: K steps with one event per step start (p50 / p90 of the
-    GPU time per step) and up to 20 steps with events around the step's
-    launch (`kernel_in_step_ms`)."""
+    With a graph (the default): the K steps — and a chained episode's closing
+    flush — are captured once into ONE graph (one replay call: the least host
+    launch overhead in a short timed region), replayed untimed until ~300
+    steps have run (the GPU's clocks ramp over the first few hundred
+    launches), then replayed ONCE between barrier + sync on both sides (host
+    clock: `elapsed`, the value's denominator) with HIP events around the
+    replay on the launch stream.  `kernel_timed_ms` = (that event time - the
+    closing flush's own duration, measured eagerly afterwards) / K: the device
+    time per step launch inside the timed region (for chained steps the
+    chained kernel back to back — the roofline's denominator).  Then, eagerly:
+    K steps with one event per step start (p50 / p90 of the GPU time per step)
+    and up to 20 steps with events around the step's launch
+    (`kernel_in_step_ms`)."""
     import torch
     import torch.distributed as dist
     from diplomjourney_amd.episode import percentile
@@ -968,42 +970,36 @@ def run_steps(args, ep, pool, use_graph, world, device):
         step(i)
     flush()
     torch.cuda.synchronize()
-    gA = gB = None
+    graph = None
     if use_graph:
         n0 = ep.steps_enqueued
         try:
-            gA = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gA):
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
                 for i in range(args.steps):
                     step(i)
-            if getattr(ep, "_pending", None) is not None:
-                gB = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gB):
-                    flush()                  # the K-th step completes in graph B
+                flush()                      # the K-th step completes inside the graph
         except Exception as e:   # capture refused (e.g. by the collective): launch eagerly
             print(f"bench: graph capture failed ({type(e).__name__}: {e}); eager launches",
                   file=sys.stderr, flush=True)
-            gA = gB = None
+            graph = None
             if hasattr(ep, "_pending"):
                 ep._pending = None           # the captured launches never ran
             torch.cuda.synchronize()
         ep.steps_enqueued = n0               # captured, not run
 
-    def replay():
-        gA.replay()
-        if gB is not None:
-            gB.replay()
-        ep.steps_enqueued += args.steps
-
-    # untimed: the clock ramp (graph replays, or eager steps)
-    ran = 0
-    while ran < 300:
-        if gA is not None:
-            replay()
+    def run_k():
+        if graph is not None:
+            graph.replay()
+            ep.steps_enqueued += args.steps
         else:
             for i in range(args.steps):
                 step(i)
             flush()
+
+    ran = 0
+    while ran < 300:                         # untimed: the clock ramp
+        run_k()
         ran += args.steps
     torch.cuda.synchronize()
     if world > 1:
@@ -1012,22 +1008,13 @@ def run_steps(args, ep, pool, use_graph, world, device):
     e0, e1 = Ev(), Ev()
     t0 = time.perf_counter()
     e0.record()
-    if gA is not None:
-        gA.replay()
-        e1.record()
-        if gB is not None:
-            gB.replay()
-        ep.steps_enqueued += args.steps
-    else:
-        for i in range(args.steps):
-            step(i)
-        e1.record()
-        flush()
+    run_k()
+    e1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_timed_ms = e0.elapsed_time(e1) / args.steps
+    timed_ms = e0.elapsed_time(e1)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1043,15 +1030,23 @@ def run_steps(args, ep, pool, use_graph, world, device):
     flush()
     torch.cuda.synchronize()
     step_gpu_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)]
-    # the step's launch inside eager steps, events around it
+    # the step's launch inside eager steps, events around it; and the closing
+    # flush's own duration (a pending chained step completed alone)
     n_kern = min(args.steps, 20)
     kern = [(Ev(), Ev()) for _ in range(n_kern)]
+    fl = [(Ev(), Ev()) for _ in range(n_kern)]
+    has_flush = False
     for i in range(n_kern):
         step(i, kern[i])
-    flush()
+        has_flush = has_flush or getattr(ep, "_pending", None) is not None
+        fl[i][0].record()
+        flush()
+        fl[i][1].record()
     torch.cuda.synchronize()
-    return {"elapsed": elapsed, "graph": gA is not None,
-            "kernel_timed_ms": kernel_timed_ms,
+    flush_ms = (sum(a.elapsed_time(b) for a, b in fl) / n_kern) if has_flush else 0.0
+    return {"elapsed": elapsed, "graph": graph is not None,
+            "kernel_timed_ms": max(timed_ms - flush_ms, 0.0) / args.steps,
+            "flush_ms": flush_ms,
             "p50_ms": percentile(step_gpu_ms, 50),
             "p90_ms": percentile(step_gpu_ms, 90),
             "kernel_in_step_ms": sum(a.elapsed_time(b) for a, b in kern) / len(kern)}
