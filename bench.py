@@ -84,9 +84,10 @@ WORKLOADS["G"] = dict(n_steps=3, per_gpu=None, robots=1000,
                            "S1 = 5 x 13 controls (274,625 leaves per robot-step)")
 FP64_VECTOR_PEAK_TFLOPS = 78.6   # MI355X spec (2 x 32 lanes x 2 flops/clk/SIMD at 2.4 GHz / 2)
 # fp64 operations per full-tree leaf (csrc/mpc_fulltree.h, one layer step + criterion), as
-# written: rect+rot 34 (heading add 1, rotation 8, two fused position updates 4, criterion 21);
-# qk21 adds 2 x 22 per leaf (two 21-node Kronrod sums + scaling).
-FT_FLOPS_PER_LEAF = {"rect+rot": 34, "rect": 34, "qk21+rot": 78, "qk21": 78}
+# written (an fma = 2): rect+rot 29 (heading add 1, rotation 6, two fused position updates 4,
+# criterion 18 with its per-problem terms folded, ft_crit); qk21 adds 2 x 22 per leaf (two
+# 21-node Kronrod sums + scaling).
+FT_FLOPS_PER_LEAF = {"rect+rot": 29, "rect": 29, "qk21+rot": 73, "qk21": 73}
 
 
 def parse():
@@ -1190,7 +1191,7 @@ def traffic_summary(traffic_json, kernel, bytes_launch, layout="soa"):
 VALU_JSON = {("k_episode_chain", "rect+cum"): ("r04_final/valu/chain.json", 1_000_000, 10),
              ("k_rollout_argmin_stream", "qk21"): ("r04_final/valu/qk21.json", 1_000_000, 10),
              ("k_rollout_generated", "rect+cum"): ("r04_final/valu/gen.json", 1_000_000, 10),
-             ("k_ft_leaves", "rect+rot"): ("r04_final/valu/ft.json", 451 ** 3, 3),
+             ("k_ft_leaves", "rect+rot"): ("r05/valu/ft.json", 451 ** 3, 3),
              # the device-resident episode drivers: the whole run is ONE launch;
              # keyed (episodes, max_calls) of workloads R and G as the bench runs them
              ("k_episodes_run", "qk21"): ("r05/valu/episodes_R.json", 1000, 1000),

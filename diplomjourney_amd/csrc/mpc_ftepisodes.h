@@ -88,7 +88,7 @@ __global__ __launch_bounds__(kBlock, kFtEpWaves) void k_ft_episodes_run(
   __shared__ int s_run;
   if (threadIdx.x == 0) s_e = eps[r];
   const int64_t s1 = static_cast<int64_t>(nv) * nb;
-  const int64_t n_items = ((s1 * s1 + 63) / 64) * ((s1 + kFtChunk - 1) / kFtChunk);
+  const int64_t n_items = ft_units(s1);
   const int64_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (int call = 0; call < max_calls; ++call) {
     if (threadIdx.x == 0) {   // the loop's head (:261) and the caller's limit
@@ -127,9 +127,9 @@ __global__ __launch_bounds__(kBlock, kFtEpWaves) void k_ft_episodes_run(
       const double w = K.L_pow2 ? u.v * K.inv_L : u.v / K.L;
       u.dphi = heading_incr<INTEG>(w, trig::tan_fast(u.beta), K);
       if (fabs(u.dphi) <= trig::kRotMax) {
-        trig::rotation_factors(u.dphi, u.sd, u.cm1);
+        trig::rotation_sc(u.dphi, u.sd, u.cd);
       } else {
-        u.sd = u.cm1 = 0.0;
+        u.sd = u.cd = 0.0;
         wide = true;
       }
       s_ctl[k] = u;
@@ -140,11 +140,11 @@ __global__ __launch_bounds__(kBlock, kFtEpWaves) void k_ft_episodes_run(
     const bool rot = ROT && !any_wide;
     uint64_t best_k = ~0ull;
     int64_t best_i = INT64_MAX;
+    const FtCrit F = ft_crit(K, atan_t);
     if (rot)
-      ft_leaves_body<INTEG, true>(K, atan_t, s_ctl, s1, 0, n_items, best_k, best_i, wave, kWaves);
+      ft_leaves_body<INTEG, true>(K, F, s_ctl, s1, 0, n_items, best_k, best_i, wave, kWaves);
     else
-      ft_leaves_body<INTEG, false>(K, atan_t, s_ctl, s1, 0, n_items, best_k, best_i, wave,
-                                   kWaves);
+      ft_leaves_body<INTEG, false>(K, F, s_ctl, s1, 0, n_items, best_k, best_i, wave, kWaves);
     block_argmin(best_k, best_i);
     if (threadIdx.x == 0) {   // the update of run_batched (run_math_model.py)
       FtEpisode& E = s_e;

@@ -11,13 +11,13 @@
 //                   all three layers: one quad window per call), the rotation
 //                   factors of dphi, v*h; a launch-wide flag when some
 //                   |dphi| > kRotMax (the rotation form is then not used)
-//   k_ft_leaves     work items = (64 consecutive (k0, k1) pairs, chunk of k2);
-//                   a shard owns a contiguous item range.  A wave takes an
-//                   item, one pair per lane: each lane derives its pair's layer-0 and
-//                   layer-1 states once, then runs the chunk with the control
-//                   of k2 WAVE-UNIFORM (scalar loads, no per-leaf vector
-//                   memory traffic); lexicographic (cost, j) arg-min per lane
-//                   -> wave -> block record
+//   k_ft_leaves     work units = (group of 64 consecutive (k0, k1) pairs, k2);
+//                   a shard owns a contiguous unit range, each wave an equal
+//                   contiguous share of it, one pair per lane: each lane derives
+//                   its pair's layer-0 and layer-1 states once per group, then
+//                   runs its k2 with the control WAVE-UNIFORM (scalar loads, no
+//                   per-leaf vector memory traffic); lexicographic (cost, j)
+//                   arg-min per lane -> wave -> block record
 //   k_ft_finalize   record reduction, the winner's three layers re-derived
 //                   with the same functions
 #pragma once
@@ -27,7 +27,7 @@
 namespace mpc {
 
 struct FtCtl {
-  double v, beta, dphi, sd, cm1;
+  double v, beta, dphi, sd, cd;   // sd, cd = sin / cos of dphi (ROT)
   double vh;   // v * h (RECT's position increment factor, formed once per control)
 };
 
@@ -35,21 +35,48 @@ struct FtState {
   double x, y, ph, s, c;
 };
 
-// criterion of run_math_model.py:82-86: 10000*dist_target (:64-65)
-// + 10*(arctan(x_t/y_t) - phi)^2 + 100*dist_line^2 (:53-61), in that order.
-MPC_HD __forceinline__ double cost_fulltree(double x, double y, double ph, const Consts& K,
-                                           double atan_t) {
-  const double a = atan_t - ph;
-  const double ex = K.x_t - x, ey = K.y_t - y;
-  const double dist_target = crit_sqrt(ex * ex + ey * ey);
-  const double dl = fabs(K.A * x - K.B * y + K.C1 - K.C2) * K.inv_den;   // (mpc_device.h cost)
-  const double d = (x == K.x_0 && y == K.y_0) ? 1000.0 : dl;
-  return 10000.0 * dist_target + 10.0 * (a * a) + 100.0 * (d * d);
+// The criterion's per-problem terms, folded once per problem (ft_crit) so that
+// a leaf spends 27 VALU on it instead of 35:
+//   10000*dist_target + 10*(arctan(x_t/y_t) - phi)^2 + 100*dist_line^2
+// (run_math_model.py:82-86) with dist_line = |A x - B y + C1 - C2| / hyp
+// (:53-61) evaluated as lin = fma(A, x, fma(-B, y, C1 - C2)) and
+// 100*dist_line^2 = (lin * K2) * lin, K2 = 100 / hyp^2; the sum as
+// fma(10000, dist_target, fma(lin * K2, lin, (10 a) a)).  Other roundings than
+// the script's order (a few ulps of the cost; the tests' 1e-12 bar).  The
+// line-origin sentinel (:57-58, dist_line = 1000) replaces lin by
+// S = sqrt(1e8 / K2): its term is 1e8 to within an ulp or two, and such a
+// leaf (the state AT the line origin, cost >= 1e8) never wins.
+struct FtCrit {
+  double x_t, y_t, x_0, y_0, A, nB, C, K2, S, atan_t;
+};
+
+MPC_HD __forceinline__ FtCrit ft_crit(const Consts& K, double atan_t) {
+  FtCrit F;
+  F.x_t = K.x_t;
+  F.y_t = K.y_t;
+  F.x_0 = K.x_0;
+  F.y_0 = K.y_0;
+  F.A = K.A;
+  F.nB = -K.B;
+  F.C = K.C1 - K.C2;
+  F.K2 = 100.0 * (K.inv_den * K.inv_den);
+  F.S = sqrt(1e8 / F.K2);
+  F.atan_t = atan_t;
+  return F;
+}
+
+MPC_HD __forceinline__ double cost_fulltree(double x, double y, double ph, const FtCrit& F) {
+  const double a = F.atan_t - ph;
+  const double ex = F.x_t - x, ey = F.y_t - y;
+  const double dist_target = crit_sqrt(fma(ex, ex, ey * ey));
+  const double lin0 = fma(F.A, x, fma(F.nB, y, F.C));
+  const double lin = (x == F.x_0 && y == F.y_0) ? F.S : lin0;
+  return fma(10000.0, dist_target, fma(lin * F.K2, lin, (a * 10.0) * a));
 }
 
 // iteration_of_predict (:111-115) with a precomputed control: heading first,
 // then the position with the new heading.  ROT: (s, c) rotated by the
-// control's factors instead of sin/cos of the new heading.
+// control's sin / cos (the candidate rollout's complex product, 4 VALU).
 template <int INTEG, bool ROT>
 MPC_HD __forceinline__ FtState ft_apply(const FtState& in, const FtCtl& u, const Consts& K) {
   FtState o;
@@ -57,7 +84,7 @@ MPC_HD __forceinline__ FtState ft_apply(const FtState& in, const FtCtl& u, const
   if constexpr (ROT) {
     o.s = in.s;
     o.c = in.c;
-    trig::rotate_by(u.sd, u.cm1, o.s, o.c);
+    trig::rotate_sc(u.sd, u.cd, o.s, o.c);
   } else {
     trig::sincos_fast(o.ph, &o.s, &o.c);
   }
@@ -85,32 +112,46 @@ __global__ __launch_bounds__(kBlock) void k_ft_controls(Consts K, const double* 
   const double w = K.L_pow2 ? u.v * K.inv_L : u.v / K.L;
   u.dphi = heading_incr<INTEG>(w, trig::tan_fast(u.beta), K);
   if (fabs(u.dphi) <= trig::kRotMax) {
-    trig::rotation_factors(u.dphi, u.sd, u.cm1);
+    trig::rotation_sc(u.dphi, u.sd, u.cd);
   } else {
-    u.sd = u.cm1 = 0.0;
+    u.sd = u.cd = 0.0;
     atomicOr(no_rot, 1u);
   }
   ctl[k] = u;
 }
 
-constexpr int kFtChunk = 256;  // k2 per wave-item
-constexpr int kFtWaves = 7;    // launch bound (waves per SIMD): <= 72 VGPRs, no scratch (8 spills)
+constexpr int kFtWaves = 7;    // launch bound (waves per SIMD): <= 72 VGPRs, no scratch
 
-// wave / n_waves: this wave's rank among the waves that share the items (the
-// launch's waves; a block's own in the device-resident episodes)
+// Work units: u = g * S1 + k2 — group g of 64 consecutive (k0, k1) pairs (one
+// per lane), control k2 of the last layer.  A launch (or shard, or robot) owns
+// the contiguous range [u_lo, u_hi); wave `wave` of `n_waves` takes an equal
+// contiguous share of it (+-1 unit).  Round 4 dealt whole (group, 256-k2
+// chunk) items round-robin: at S1 = 451 that was one item per wave with the
+// 256- and 195-k2 chunks landing on alternate SIMDs and 6 or 7 waves per
+// SIMD — the launch waited on its most loaded SIMDs.
+__host__ __device__ __forceinline__ int64_t ft_units(int64_t s1) {
+  return ((s1 * s1 + 63) / 64) * s1;
+}
+
+// wave / n_waves: this wave's rank among the waves that share [u_lo, u_hi)
+// (the launch's waves; a block's own in the device-resident episodes)
 template <int INTEG, bool ROT>
-__device__ __forceinline__ void ft_leaves_body(const Consts& K, double atan_t,
+__device__ __forceinline__ void ft_leaves_body(const Consts& K, const FtCrit& F,
                                                const FtCtl* __restrict__ ctl, int64_t s1,
-                                               int64_t item_lo, int64_t item_hi,
+                                               int64_t u_lo, int64_t u_hi,
                                                uint64_t& best_k, int64_t& best_i, int64_t wave,
                                                int64_t n_waves) {
   const int lane = threadIdx.x & 63;
   const int64_t n_pairs = s1 * s1;
-  const int64_t n_chunks = (s1 + kFtChunk - 1) / kFtChunk;
+  const int64_t total = u_hi - u_lo, share = total / n_waves, rem = total % n_waves;
+  int64_t u = u_lo + wave * share + (wave < rem ? wave : rem);
+  const int64_t u_end = u + share + (wave < rem ? 1 : 0);
   double best_c = key_cost(best_k);   // (+inf: none yet)
-  for (int64_t item = item_lo + wave; item < item_hi; item += n_waves) {
-    const int64_t g = item / n_chunks;
-    const int64_t c = item - g * n_chunks;
+  while (u < u_end) {   // wave-uniform
+    const int64_t g = u / s1;
+    const int64_t k2_lo = u - g * s1;
+    const int64_t k2_hi = (s1 - k2_lo < u_end - u) ? s1 : k2_lo + (u_end - u);
+    u += k2_hi - k2_lo;
     const int64_t m = g * 64 + lane;           // this lane's (k0, k1) pair
     const bool live = m < n_pairs;
     const int64_t mm = live ? m : n_pairs - 1;
@@ -118,21 +159,19 @@ __device__ __forceinline__ void ft_leaves_body(const Consts& K, double atan_t,
     const FtState s0{K.x, K.y, K.phi, K.s0, K.c0};
     const FtState l0 = ft_apply<INTEG, ROT>(s0, ctl[k0], K);
     const FtState l1 = ft_apply<INTEG, ROT>(l0, ctl[k1], K);
-    const int64_t k2_lo = c * kFtChunk;
-    const int64_t k2_hi = k2_lo + kFtChunk < s1 ? k2_lo + kFtChunk : s1;
     const int64_t j0 = mm * s1;
 #ifndef MPC_FT_UNROLL
 #define MPC_FT_UNROLL 4   // k2 iterations interleaved (A/B: 1 -> 2 -> 4 = 353 -> 337 -> 335 us per config-F step)
 #endif
-    // the item's best k2 (32-bit; -1: none), its leaf index formed once per item
+    // the piece's best k2 (32-bit; -1: none), its leaf index formed once per piece
     int32_t best_k2 = -1;
 #pragma unroll MPC_FT_UNROLL
     for (int64_t k2 = k2_lo; k2 < k2_hi; ++k2) {   // wave-uniform control
-      const FtCtl u = ctl[k2];
-      const FtState lf = ft_apply<INTEG, ROT>(l1, u, K);
-      const double c = cost_fulltree(lf.x, lf.y, lf.ph, K, atan_t);
-      // a lane's leaf indices only grow (items ascend, and so do (k0, k1) and
-      // k2 within them): strict < keeps its first minimum, as rec_less would.
+      const FtCtl uc = ctl[k2];
+      const FtState lf = ft_apply<INTEG, ROT>(l1, uc, K);
+      const double c = cost_fulltree(lf.x, lf.y, lf.ph, F);
+      // a lane's leaf indices only grow (units ascend: (k0, k1) with g, and
+      // k2 within a group): strict < keeps its first minimum, as rec_less would.
       // Compared as doubles: the criterion is >= 0, where the double order is
       // the cost keys' (+-0 equal, +inf and NaN never below a best), so the
       // key is formed once per lane instead of per leaf.
@@ -150,19 +189,18 @@ template <int INTEG, bool ROT>
 __global__ __launch_bounds__(kBlock, kFtWaves) void k_ft_leaves(Consts K, double atan_t,
                                                       const FtCtl* __restrict__ ctl,
                                                       const uint32_t* __restrict__ no_rot,
-                                                      int64_t s1, int64_t item_lo,
-                                                      int64_t item_hi, Rec* __restrict__ part) {
+                                                      int64_t s1, int64_t u_lo,
+                                                      int64_t u_hi, Rec* __restrict__ part) {
   uint64_t best_k = ~0ull;
   int64_t best_i = INT64_MAX;
   const int64_t wave = static_cast<int64_t>(blockIdx.x) * kWaves +
                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t n_waves = static_cast<int64_t>(gridDim.x) * kWaves;
+  const FtCrit F = ft_crit(K, atan_t);
   if (ROT && *no_rot == 0u)
-    ft_leaves_body<INTEG, true>(K, atan_t, ctl, s1, item_lo, item_hi, best_k, best_i, wave,
-                                n_waves);
+    ft_leaves_body<INTEG, true>(K, F, ctl, s1, u_lo, u_hi, best_k, best_i, wave, n_waves);
   else
-    ft_leaves_body<INTEG, false>(K, atan_t, ctl, s1, item_lo, item_hi, best_k, best_i, wave,
-                                 n_waves);
+    ft_leaves_body<INTEG, false>(K, F, ctl, s1, u_lo, u_hi, best_k, best_i, wave, n_waves);
   block_argmin(best_k, best_i);
   if (threadIdx.x == 0) part[blockIdx.x] = Rec{best_k, best_i};
 }
@@ -255,16 +293,17 @@ __global__ __launch_bounds__(kBlock, kFtWaves) void k_ft_leaves_batched(
   const int r = blockIdx.y;
   const Consts K = robots[r].K;
   const double atan_t = robots[r].atan_t;
-  const int64_t n_items = ((s1 * s1 + 63) / 64) * ((s1 + kFtChunk - 1) / kFtChunk);
+  const int64_t n_items = ft_units(s1);
   uint64_t best_k = ~0ull;
   int64_t best_i = INT64_MAX;
   const int64_t wave = static_cast<int64_t>(blockIdx.x) * kWaves +
                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t n_waves = static_cast<int64_t>(gridDim.x) * kWaves;
+  const FtCrit F = ft_crit(K, atan_t);
   if (ROT && *no_rot == 0u)
-    ft_leaves_body<INTEG, true>(K, atan_t, ctl, s1, 0, n_items, best_k, best_i, wave, n_waves);
+    ft_leaves_body<INTEG, true>(K, F, ctl, s1, 0, n_items, best_k, best_i, wave, n_waves);
   else
-    ft_leaves_body<INTEG, false>(K, atan_t, ctl, s1, 0, n_items, best_k, best_i, wave, n_waves);
+    ft_leaves_body<INTEG, false>(K, F, ctl, s1, 0, n_items, best_k, best_i, wave, n_waves);
   block_argmin(best_k, best_i);
   if (threadIdx.x == 0) part[static_cast<int64_t>(r) * gridDim.x + blockIdx.x] =
       Rec{best_k, best_i};

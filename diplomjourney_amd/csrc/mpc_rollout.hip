@@ -1094,6 +1094,22 @@ int mpc_episodes_run(void* state, int32_t n_robots, int32_t n_steps, int32_t int
 // ----------------------------- full tree -----------------------------------
 static size_t ft_align(size_t n) { return (n + 255) & ~static_cast<size_t>(255); }
 static constexpr int64_t kFtMaxBlocks = 2048;
+static constexpr int64_t kFtMinShare = 32;   // work units per wave at least (small trees)
+
+// The current device's CU count (cached per device).
+static int64_t device_cus() {
+  static int64_t cache[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+  if (cache[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus < 1)
+      cus = 256;
+    cache[dev] = cus;
+  }
+  return cache[dev];
+}
 
 size_t mpc_fulltree_workspace_bytes(int32_t n_v, int32_t n_beta) {
   if (n_v < 1 || n_beta < 1) return 0;
@@ -1129,19 +1145,23 @@ int mpc_fulltree_argmin(const mpc_fulltree_problem_t* p, const double* v_grid, i
   Rec* part = reinterpret_cast<Rec*>(w + ft_align(s1 * sizeof(FtCtl)) + 256);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (hipMemsetAsync(no_rot, 0, sizeof(uint32_t), st) != hipSuccess) return MPC_ERR_HIP;
-  const int64_t n_items = cdiv(s1 * s1, 64) * cdiv(s1, kFtChunk);
-  const int64_t base = n_items / n_shards, rem = n_items % n_shards;
-  const int64_t item_lo = shard * base + std::min<int64_t>(shard, rem);
-  const int64_t item_hi = item_lo + base + (shard < rem ? 1 : 0);
-  const int64_t grid =
-      std::max<int64_t>(1, std::min(cdiv(item_hi - item_lo, kWaves), kFtMaxBlocks));
+  // the shard's contiguous range of work units (ft_units), shared out evenly
+  // over a grid of kFtWaves blocks per CU (one wave per SIMD each: every SIMD
+  // holds the same number of equal shares), fewer for a small tree
+  const int64_t n_units = ft_units(s1);
+  const int64_t base = n_units / n_shards, rem = n_units % n_shards;
+  const int64_t u_lo = shard * base + std::min<int64_t>(shard, rem);
+  const int64_t u_hi = u_lo + base + (shard < rem ? 1 : 0);
+  const int64_t grid = std::max<int64_t>(
+      1, std::min({cdiv(u_hi - u_lo, kWaves * kFtMinShare), device_cus() * kFtWaves,
+                   kFtMaxBlocks}));
   dispatch_mode2(integrator, [&](auto integ, auto rot) {
     constexpr int I = decltype(integ)::value;
     constexpr bool R = decltype(rot)::value;
     k_ft_controls<I><<<cdiv(s1, kBlock), kBlock, 0, st>>>(K, v_grid, beta_grid, n_beta, s1, ctl,
                                                           no_rot);
-    k_ft_leaves<I, R><<<grid, kBlock, 0, st>>>(K, p->atan_target, ctl, no_rot, s1, item_lo,
-                                                item_hi, part);
+    k_ft_leaves<I, R><<<grid, kBlock, 0, st>>>(K, p->atan_target, ctl, no_rot, s1, u_lo, u_hi,
+                                                part);
     k_ft_finalize<I, R><<<1, kFinBlock, 0, st>>>(part, static_cast<int>(grid), K, ctl, no_rot,
                                                  s1, incumbent, out);
   });
@@ -1149,10 +1169,9 @@ int mpc_fulltree_argmin(const mpc_fulltree_problem_t* p, const double* v_grid, i
 }
 
 static int64_t ft_blocks_per_robot(int64_t s1, int32_t n) {
-  const int64_t n_items = cdiv(s1 * s1, 64) * cdiv(s1, kFtChunk);
   // about 4096 blocks in total, at least one per robot
   const int64_t want = std::max<int64_t>(1, 4096 / std::max<int32_t>(n, 1));
-  return std::max<int64_t>(1, std::min(cdiv(n_items, kWaves), want));
+  return std::max<int64_t>(1, std::min(cdiv(ft_units(s1), kWaves * kFtMinShare), want));
 }
 
 size_t mpc_fulltree_batched_workspace_bytes(int32_t n_problems, int32_t n_v, int32_t n_beta) {

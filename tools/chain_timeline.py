@@ -76,9 +76,8 @@ def build():
     patch(os.path.join(cs, "mpc_episode.h"), [
         # P2P block 0 (p2p_complete): candidate from the records, posted, the
         # world's gathered; published (advance_from_candidates' store_update)
-        ("  records_candidate(part_prev, n_part_prev, v_prev, b_prev, n_cand, n_steps, index_base, lc);\n",
-         "  records_candidate(part_prev, n_part_prev, v_prev, b_prev, n_cand, n_steps, index_base, lc);\n"
-         f"  {b0(1)}\n"),
+        ("                           lc);\n  if (static_cast<int>(threadIdx.x) < world)",
+         f"                           lc);\n  {b0(1)}\n  if (static_cast<int>(threadIdx.x) < world)"),
         ("  post_candidate(s_peers, s_rank, world, prev, slot, n_steps, lc);\n",
          f"  post_candidate(s_peers, s_rank, world, prev, slot, n_steps, lc);\n  {b0(2)}\n"),
         ("      wait_mailbox(S, mb, prev, slot, world, n_steps, s_err ? 0ull : kPeerWaitTicks);\n",
