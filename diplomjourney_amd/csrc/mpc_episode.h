@@ -65,10 +65,12 @@ static_assert(sizeof(Consts) % 4 == 0 && kPubWords <= 64, "published words: one 
 
 // EpisodeHead (mpc_kernels.h): the scalars; the grids only feed the sampler.
 // The stale trajectory follows the head (staged and stored with it as one
-// run of kStagedWords words).
+// run of kStoredWords words), then the early-publication inputs (staged with
+// both by a chained step's block 0: kStagedWords).
 struct EpisodeState {
   EpisodeHead h;
   StaleTraj st;        // right after the head: staged and stored with it
+  EarlyPub early;      // right after the stale trajectory: staged with both
   double grid_v[kEpMaxGrid];
   double grid_b[kEpMaxGrid];
   uint32_t done;       // blocks of the running fused launch that have finished
@@ -91,6 +93,7 @@ struct EpisodeState {
   alignas(128) uint64_t gathered_tag;
 };
 static_assert(offsetof(EpisodeState, st) == sizeof(EpisodeHead), "stale trajectory follows the head");
+static_assert(offsetof(EpisodeState, early) == kStoredWords * 8, "EarlyPub follows the stale trajectory");
 
 __device__ inline Consts episode_consts(const EpisodeHead& S, double x, double y, double phi,
                                         double L, double t_a, double t_b) {
@@ -154,11 +157,35 @@ __device__ inline void episode_prepare(const mpc_episode_config_t& c, EpisodeHea
   S.seed = episode_seed(c, S);
 }
 
+// The head's early_* fields (EpisodeHead): the next step's early-publication
+// inputs that do not depend on its winner — episode_advance's decisions
+// (:559-569, :542 and the step limit) as far as the head alone fixes them,
+// with st the stale trajectory the step will return without a winner.
+__device__ inline void episode_early_prepare(const mpc_episode_config_t& c, const EpisodeHead& S,
+                                             const StaleTraj& st, EarlyPub& E) {
+  E.step = S.step;
+  E.t = S.t + c.delta_t;
+  E.h = (E.t + c.delta_t) - E.t;             // consts_from_problem
+  E.hl = 0.5 * ((E.t + c.delta_t) - E.t);
+  const bool common = !(c.stop_rule == 0 && S.recursive) && S.p != c.p_turn_right &&
+                      S.p != c.p_turn_left && S.p != c.p_new_target &&
+                      !(c.max_steps > 0 && S.p + 1 > c.max_steps);
+  const int k = S.m == 2 ? 2 : (S.m == 1 ? 1 : 0);
+  E.k = common ? k : -1;
+  E.x = S.has_traj ? st.ot[k][0] : S.x;
+  E.y = S.has_traj ? st.ot[k][1] : S.y;
+  E.ph = S.has_traj ? st.ot[k][2] : S.phi;
+  E.alt = early_pose_ok(c, S, E.x, E.y) ? 1 : 0;
+}
+
 __global__ void k_episode_reset(mpc_episode_config_t c, EpisodeState* __restrict__ S) {
   if (threadIdx.x != 0) return;
   EpisodeHead H = {};
   episode_restart(c, H);
   episode_prepare(c, H);
+  EarlyPub E;
+  episode_early_prepare(c, H, S->st, E);
+  S->early = E;
   S->h = H;
   S->done = 0u;
   S->chain_error = 0u;
@@ -393,12 +420,6 @@ __device__ inline void turn_target(double ax, double ay, double aphi, double d, 
   }
 }
 
-// r.tr[k][q] for a runtime k in {0, 1, 2} by selects: a dynamically indexed
-// local array would live in scratch memory (a ~µs round trip per access).
-__device__ __forceinline__ double tr_at(const Winner& r, int k, int q) {
-  const double a = r.tr[0][q], b = r.tr[1][q], c = r.tr[2][q];
-  return k == 0 ? a : (k == 1 ? b : c);
-}
 
 // Episode._advance = the rest of math_mpc's loop body after predictive_control
 // (:542-574 with :351-429): the returned pose is the winner's layer state
@@ -418,9 +439,17 @@ __device__ __forceinline__ double tr_at(const Winner& r, int k, int q) {
 // c.stop_rule 1: run_math_model.py's stuck detector instead of math_mpc's —
 // `recursive` counts the episode's non-moving steps and the second one ends
 // it at once (:266-272, before the on-target test of the loop head).
+// early (a chained step's block 0 that published early, finalize_block):
+// the next step's Consts and t as published (8-B aligned LDS words) — the
+// step cannot end then, and the update takes t from them and leaves H.K to
+// the caller (it stores the published words as the head's constants); a
+// step that ends anyway sets *early_bad (chain error 6) and is prepared in
+// full.
 template <bool RESTART = true>
 __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeHead& H,
-                                       StaleTraj& st, const Winner& r, mpc_episode_log_t& L) {
+                                       StaleTraj& st, const Winner& r, mpc_episode_log_t& L,
+                                       const uint32_t* early = nullptr,
+                                       bool* early_bad = nullptr) {
   EpisodeHead* S = &H;
   S->steps_for_slowing -= 1;
   S->incumbent = 9223372036854775808.0;  // float(sys.maxsize), :428
@@ -531,14 +560,25 @@ __device__ inline void episode_advance(const mpc_episode_config_t& c, EpisodeHea
     if constexpr (!RESTART) return;
     episode_restart(c, *S);
   }
-  episode_prepare(c, *S);
+  if (early && (ended || reinterpret_cast<const Consts*>(early)->x != S->x ||
+                reinterpret_cast<const Consts*>(early)->y != S->y ||
+                reinterpret_cast<const Consts*>(early)->phi != S->phi))
+    *early_bad = true;   // (never expected: the early decisions are this update's)
+  if (early && !ended) {
+    // K: the published words (= episode_prepare's; the caller stores them)
+    S->t = *reinterpret_cast<const double*>(early + sizeof(Consts) / 4);
+    S->seed = episode_seed(c, *S);
+  } else {
+    episode_prepare(c, *S);
+  }
 }
 
 __device__ void episode_hook(const mpc_episode_config_t& c, const EpisodeHook& h,
                              const Winner& r, EpisodeHead& H, StaleTraj& st,
-                             mpc_episode_log_t& L, mpc_episode_log_t*& slot) {
+                             mpc_episode_log_t& L, mpc_episode_log_t*& slot,
+                             const uint32_t* early, bool* early_bad) {
   slot = log_slot(h.log, h.cap, H.step);
-  episode_advance(c, H, st, r, L);
+  episode_advance(c, H, st, r, L, early, early_bad);
 }
 
 // Multi-GPU: lexicographic (cost, global index) selection over the gathered
@@ -550,7 +590,7 @@ __device__ inline void advance_from_results(const mpc_episode_config_t& c, Episo
                                             const mpc_result_t* __restrict__ res, int n,
                                             mpc_episode_log_t* __restrict__ log, int cap,
                                             bool end_chain = true) {
-  __shared__ uint64_t s_head[kStagedWords];
+  __shared__ uint64_t s_head[kStoredWords];
   __shared__ mpc_episode_log_t s_log;
   __shared__ mpc_episode_log_t* s_slot;
   if (threadIdx.x < kStaleWords)   // the stale trajectory, staged beside the head
@@ -590,12 +630,12 @@ __device__ void advance_from_candidates(const mpc_episode_config_t& c, EpisodeSt
                                         mpc_result_t* __restrict__ out,
                                         mpc_episode_log_t* __restrict__ log, int cap,
                                         uint32_t publish_epoch, EmitLds* lds) {
-  __shared__ uint64_t s_head[kStagedWords];
+  __shared__ uint64_t s_head[kStoredWords];
   __shared__ mpc_episode_log_t s_log;
   __shared__ mpc_episode_log_t* s_slot;
   __shared__ int s_best;
   __shared__ uint64_t s_bk;
-  if (threadIdx.x < kStagedWords)
+  if (threadIdx.x < kStoredWords)
     s_head[threadIdx.x] = reinterpret_cast<const uint64_t*>(&S->h)[threadIdx.x];
   if (threadIdx.x == 0) {
     int best = 0;
@@ -1307,9 +1347,32 @@ __device__ __forceinline__ void chain_tiles(EpisodeState* __restrict__ S, uint32
           if (fin && threadIdx.x < kPubWords) s_w[threadIdx.x] = static_cast<uint32_t>(w_pre >> 32);
         }
         // (wave 0 only: its clock reads are uniform)
-        const uint32_t deadline = wall_deadline(WAIT_TICKS);
-        while (!fin && !(fin = chain_read(S, epoch, s_w, s_tag)) && !wall_passed(deadline))
-          __builtin_amdgcn_s_sleep(4);
+        // Two polls in flight, issued ~0.1 us apart: a poll's answer is as of
+        // when it reached memory, so the words are seen about half a round
+        // trip after they land instead of up to one and a half.
+        if (!fin) {
+          const uint32_t deadline = wall_deadline(WAIT_TICKS);
+          const int q = threadIdx.x;
+          uint64_t* const pw = &S->chain_pub[q < kPubWords ? q : 0];
+          auto ld = [&]() {
+            return __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          };
+          auto here = [&](uint64_t w) {
+            return __ballot(q < kPubWords && static_cast<uint32_t>(w) != epoch) == 0;
+          };
+          uint64_t a = ld(), b = 0, got = 0;
+          for (;;) {
+            __builtin_amdgcn_s_sleep(2);
+            b = ld();
+            if (here(a)) { got = a; fin = true; break; }
+            if (wall_passed(deadline)) break;
+            __builtin_amdgcn_s_sleep(2);
+            a = ld();
+            if (here(b)) { got = b; fin = true; break; }
+            if (wall_passed(deadline)) break;
+          }
+          if (fin && q < kPubWords) s_w[q] = static_cast<uint32_t>(got >> 32);
+        }
         if (!fin && threadIdx.x == 0) S->chain_error = 1u;
       }
       __syncthreads();
@@ -1380,7 +1443,7 @@ __global__ __launch_bounds__(kBlock, chain_waves<MODE>()) void k_episode_chain(
                                  n_steps, index_base, out_prev, log, cap, epoch);
       } else if constexpr (MODE == kChainFin) {
         const Consts Kp = S->h.K;
-        const EpisodeHook hook{&S->h, log, cap, S->chain_pub, kPubWords, epoch};
+        const EpisodeHook hook{&S->h, log, cap, S->chain_pub, kPubWords, epoch, &S->chain_error};
         // (block 0 never fills the control ring: its LDS holds the re-roll)
         finalize_block<INTEG, ROT, true, kBlock, false, false, TILED>(
             part_prev, n_part_prev, Kp, v_prev, b_prev, n_cand, n_steps, index_base,

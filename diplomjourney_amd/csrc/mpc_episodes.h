@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kBlock, kEpisodesWaves) void k_episodes_run(
   const int r = blockIdx.x;
   const mpc_episode_config_t& c = cfgs[r];
   RobotState* __restrict__ R = &robots[r];
-  __shared__ uint64_t s_head[kStagedWords];   // head + stale trajectory
+  __shared__ uint64_t s_head[kStoredWords];   // head + stale trajectory
   __shared__ double s_v[kEpMaxGrid], s_b[kEpMaxGrid];
   __shared__ int s_nv, s_nb, s_stop, s_calls;
   __shared__ uint64_t s_bk;
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kBlock, kEpisodesWaves) void k_episodes_run(
   __shared__ mpc_episode_log_t s_log;
   __shared__ mpc_result_t s_out;
   __shared__ EmitLds lds;
-  if (threadIdx.x < kStagedWords)
+  if (threadIdx.x < kStoredWords)
     s_head[threadIdx.x] = reinterpret_cast<const uint64_t*>(R)[threadIdx.x];
   if (threadIdx.x == 0) {
     s_stop = R->stop;
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(kBlock, kEpisodesWaves) void k_episodes_run(
           [threadIdx.x] = reinterpret_cast<const uint64_t*>(&s_log)[threadIdx.x];
   }
   __syncthreads();
-  if (threadIdx.x < kStagedWords) reinterpret_cast<uint64_t*>(R)[threadIdx.x] = s_head[threadIdx.x];
+  if (threadIdx.x < kStoredWords) reinterpret_cast<uint64_t*>(R)[threadIdx.x] = s_head[threadIdx.x];
   if (threadIdx.x == 0) {
     R->stop = s_stop;
     R->calls = s_calls;

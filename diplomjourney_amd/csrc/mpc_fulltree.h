@@ -133,8 +133,30 @@ __host__ __device__ __forceinline__ int64_t ft_units(int64_t s1) {
   return ((s1 * s1 + 63) / 64) * s1;
 }
 
+// The leaf (k0, k1, k2) of lane-pair mm and control k2 from the layer-1 state.
+template <int INTEG, bool ROT>
+__device__ __forceinline__ double ft_leaf(const FtState& l1, const FtCtl& u, const Consts& K,
+                                          const FtCrit& F) {
+  const FtState lf = ft_apply<INTEG, ROT>(l1, u, K);
+  return cost_fulltree(lf.x, lf.y, lf.ph, F);
+}
+
 // wave / n_waves: this wave's rank among the waves that share [u_lo, u_hi)
-// (the launch's waves; a block's own in the device-resident episodes)
+// (the launch's waves; a block's own in the device-resident episodes).
+// Each lane keeps the first strict minimum of its leaves — which ascend in
+// leaf index (units ascend: (k0, k1) with g, k2 within a group) — in three
+// steps, so that the per-leaf bookkeeping is 1.5 VALU instead of 3:
+//   * per 4 consecutive k2 (a quad): the quad minimum (3 fmin); if it is
+//     strictly below the lane's best, the quad's first k2 (one compare, one
+//     32-bit select) — the first quad reaching a value keeps it, as the scan
+//     would;
+//   * per piece (the wave's run of k2 within one group): the group of the best
+//     quad, if the piece improved it;
+//   * once per wave: the winning quad re-evaluated (the same operations, so the
+//     same bits) to find its first leaf at the minimum.
+// Costs are compared as doubles: the criterion is >= 0, where the double order
+// is the cost keys' (+-0 equal, +inf and NaN never below a best; fmin ignores
+// a NaN), so the key is formed once per lane.
 template <int INTEG, bool ROT>
 __device__ __forceinline__ void ft_leaves_body(const Consts& K, const FtCrit& F,
                                                const FtCtl* __restrict__ ctl, int64_t s1,
@@ -146,41 +168,53 @@ __device__ __forceinline__ void ft_leaves_body(const Consts& K, const FtCrit& F,
   const int64_t total = u_hi - u_lo, share = total / n_waves, rem = total % n_waves;
   int64_t u = u_lo + wave * share + (wave < rem ? wave : rem);
   const int64_t u_end = u + share + (wave < rem ? 1 : 0);
+  const FtState s0{K.x, K.y, K.phi, K.s0, K.c0};
   double best_c = key_cost(best_k);   // (+inf: none yet)
+  int64_t best_mm = -1;               // the pair of the lane's best quad (-1: best_i stands)
+  int32_t best_q = 0;                 // ... and its first k2
   while (u < u_end) {   // wave-uniform
     const int64_t g = u / s1;
     const int64_t k2_lo = u - g * s1;
     const int64_t k2_hi = (s1 - k2_lo < u_end - u) ? s1 : k2_lo + (u_end - u);
     u += k2_hi - k2_lo;
     const int64_t m = g * 64 + lane;           // this lane's (k0, k1) pair
-    const bool live = m < n_pairs;
-    const int64_t mm = live ? m : n_pairs - 1;
+    const int64_t mm = m < n_pairs ? m : n_pairs - 1;
     const int64_t k0 = mm / s1, k1 = mm - k0 * s1;
-    const FtState s0{K.x, K.y, K.phi, K.s0, K.c0};
     const FtState l0 = ft_apply<INTEG, ROT>(s0, ctl[k0], K);
     const FtState l1 = ft_apply<INTEG, ROT>(l0, ctl[k1], K);
-    const int64_t j0 = mm * s1;
-#ifndef MPC_FT_UNROLL
-#define MPC_FT_UNROLL 4   // k2 iterations interleaved (A/B: 1 -> 2 -> 4 = 353 -> 337 -> 335 us per config-F step)
-#endif
-    // the piece's best k2 (32-bit; -1: none), its leaf index formed once per piece
-    int32_t best_k2 = -1;
-#pragma unroll MPC_FT_UNROLL
-    for (int64_t k2 = k2_lo; k2 < k2_hi; ++k2) {   // wave-uniform control
-      const FtCtl uc = ctl[k2];
-      const FtState lf = ft_apply<INTEG, ROT>(l1, uc, K);
-      const double c = cost_fulltree(lf.x, lf.y, lf.ph, F);
-      // a lane's leaf indices only grow (units ascend: (k0, k1) with g, and
-      // k2 within a group): strict < keeps its first minimum, as rec_less would.
-      // Compared as doubles: the criterion is >= 0, where the double order is
-      // the cost keys' (+-0 equal, +inf and NaN never below a best), so the
-      // key is formed once per lane instead of per leaf.
-      // (c >= +0, never -0: the minimum of the doubles is the better one; a
-      // NaN c leaves best_c)
-      if (c < best_c) best_k2 = static_cast<int32_t>(k2);
+    int32_t q = -1;   // the piece's best quad (first k2; -1: none)
+    int64_t k2 = k2_lo;
+    for (; k2 + 4 <= k2_hi; k2 += 4) {   // wave-uniform controls
+      const double c0 = ft_leaf<INTEG, ROT>(l1, ctl[k2], K, F);
+      const double c1 = ft_leaf<INTEG, ROT>(l1, ctl[k2 + 1], K, F);
+      const double c2 = ft_leaf<INTEG, ROT>(l1, ctl[k2 + 2], K, F);
+      const double c3 = ft_leaf<INTEG, ROT>(l1, ctl[k2 + 3], K, F);
+      const double cm = fmin(fmin(c0, c1), fmin(c2, c3));
+      if (cm < best_c) q = static_cast<int32_t>(k2);
+      best_c = fmin(best_c, cm);
+    }
+    for (; k2 < k2_hi; ++k2) {   // the piece's last < 4 leaves: quads of one
+      const double c = ft_leaf<INTEG, ROT>(l1, ctl[k2], K, F);
+      if (c < best_c) q = static_cast<int32_t>(k2);
       best_c = fmin(best_c, c);
     }
-    if (best_k2 >= 0) best_i = j0 + best_k2;
+    if (q >= 0) {
+      best_mm = mm;
+      best_q = q;
+    }
+  }
+  if (__ballot(best_mm >= 0) != 0) {   // the winning quad's first leaf at best_c
+    if (best_mm >= 0) {
+      const int64_t k0 = best_mm / s1, k1 = best_mm - k0 * s1;
+      const FtState l0 = ft_apply<INTEG, ROT>(s0, ctl[k0], K);
+      const FtState l1 = ft_apply<INTEG, ROT>(l0, ctl[k1], K);
+      // (a quad of one — a piece's last leaves — matches at j = 0: the scan
+      // never reaches past its quad)
+      int32_t hit = -1;
+      for (int32_t j = 0; j < 4 && hit < 0 && best_q + j < s1; ++j)
+        if (ft_leaf<INTEG, ROT>(l1, ctl[best_q + j], K, F) == best_c) hit = best_q + j;
+      best_i = best_mm * s1 + (hit >= 0 ? hit : best_q);   // (hit >= 0: same bits)
+    }
   }
   best_k = cost_key_nonneg(best_c);   // (+inf: ~0, no finite leaf)
 }

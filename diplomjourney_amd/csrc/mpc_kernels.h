@@ -589,6 +589,13 @@ struct Winner {
   double tr[3][3];     // states of steps 0..2 (clamped to the horizon)
 };
 
+// r.tr[k][q] for a runtime k in {0, 1, 2} by selects: a dynamically indexed
+// local array would live in scratch memory (a ~µs round trip per access).
+__device__ __forceinline__ double tr_at(const Winner& r, int k, int q) {
+  const double a = r.tr[0][q], b = r.tr[1][q], c = r.tr[2][q];
+  return k == 0 ? a : (k == 1 ? b : c);
+}
+
 // Re-roll the winner and fill the result record.  Called by ALL threads of
 // the block once thread 0 holds the winner (key, col).  The N-step recurrence
 // is split so that only cheap accumulations stay serial: lane s computes the
@@ -618,13 +625,23 @@ __device__ __forceinline__ EmitLds* ring_lds() {
   return reinterpret_cast<EmitLds*>(&g_ring[0][0][0][0]);
 }
 
-template <int INTEG, int ROT>
+// Side work for the threads that have no part in a phase of the re-roll (every
+// thread >= 64: n_steps <= 32): side_a() runs beside the per-step factors,
+// side_b(fast) beside lane 0's serial pass; both are called by every thread
+// and pick their own threads.
+struct NoSide {
+  __device__ void operator()() const {}
+  __device__ void operator()(bool) const {}
+};
+
+template <int INTEG, int ROT, class SideA = NoSide, class SideB = NoSide>
 __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
                             const double* __restrict__ b, int64_t ld, int n_steps, uint64_t key,
                             int64_t col, int64_t reported_index, double incumbent,
                             mpc_result_t* __restrict__ out, EmitLds* lds, Winner* win = nullptr,
                             const double* pre_v = nullptr, const double* pre_b = nullptr,
-                            bool defer_tail = false) {
+                            bool defer_tail = false, const SideA& side_a = SideA{},
+                            const SideB& side_b = SideB{}) {
   double* s_v = lds->v;
   double* s_dphi = lds->dphi;
   double* s_phi = lds->phi;
@@ -670,6 +687,7 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
       s_c[lane] = rc;
     }
   }
+  side_a();
   __syncthreads();
   // Regular rotation-mode winner: ONE serial pass on lane 0 (heading, rotation,
   // position); every other case keeps the heading chain / sincos phases.
@@ -788,6 +806,7 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
       }
     }
   }
+  side_b(fast);
   __syncthreads();
   if (valid && lane < 3 * lds->tail_from) (&out->traj[0][0])[lane] = s_tr[lane];
 }
@@ -849,6 +868,22 @@ struct StaleTraj {
   double v, beta;
 };
 
+// What a chained step's early publication needs of the update it makes,
+// formed when the previous step's update is done (episode_early_prepare):
+// the finishing layer k when the step can only be a common one (no event,
+// break or limit; -1 otherwise), the next step's t and step sizes, and the
+// pose a step without winner returns (stale layer k, or the pose) and whether
+// it passes the end-of-step checks.  `step`: the head's
+// step count it was formed for (a step completed by another path leaves it
+// stale, and the next chained step then publishes after its update).
+// Stored right after StaleTraj, staged with the head.
+struct EarlyPub {
+  int64_t step;
+  int32_t k, alt;
+  double t, h, hl;
+  double x, y, ph;   // (its sin / cos are evaluated when used: a step without winner is rare)
+};
+
 struct EpisodeHook {  // single-GPU episode: finalize also advances it
   EpisodeHead* H;     // nullptr: no hook
   mpc_episode_log_t* log;
@@ -856,10 +891,13 @@ struct EpisodeHook {  // single-GPU episode: finalize also advances it
   uint64_t* chain_pub = nullptr;   // cleared with the update (ends a chain of chained steps) ...
   int chain_pub_words = 0;
   uint32_t publish_epoch = 0;      // ... or, nonzero, the next step's constants published
+  uint32_t* chain_error = nullptr; // (publish_epoch: the early publication's self-check, code 6)
 };
 constexpr int kHeadWords = static_cast<int>(sizeof(EpisodeHead) / 8);
 constexpr int kStaleWords = static_cast<int>(sizeof(StaleTraj) / 8);
-constexpr int kStagedWords = kHeadWords + kStaleWords;   // head + stale trajectory
+constexpr int kEarlyWords = static_cast<int>(sizeof(EarlyPub) / 8);
+constexpr int kStoredWords = kHeadWords + kStaleWords;   // head + stale trajectory
+constexpr int kStagedWords = kStoredWords + kEarlyWords; // ... + the early-publication inputs
 static_assert(kStagedWords <= 64, "staged head: one word per lane");
 constexpr int kLogWords = static_cast<int>(sizeof(mpc_episode_log_t) / 8);
 static_assert(sizeof(EpisodeHead) % 8 == 0 && kHeadWords <= 64, "head: one word per lane");
@@ -878,12 +916,15 @@ __device__ __forceinline__ mpc_episode_log_t* log_slot(mpc_episode_log_t* log, i
 // layout of EpisodeState::chain_pub: Consts' dwords, then t's two) straight
 // from the LDS copy — not re-read from HBM after the head's stores, which
 // would put a store drain and a load round trip in front of the publication.
+// published: the head's Consts are the published words `pub` (the early
+// publication's), not s_head's.
 __device__ __forceinline__ void store_update(EpisodeHead* H, const uint64_t* s_head,
                                              mpc_episode_log_t* slot, const uint64_t* s_log,
                                              uint64_t* chain_pub, int chain_words,
-                                             uint32_t epoch = 0) {
+                                             uint32_t epoch = 0, bool published = false,
+                                             const uint32_t* pub = nullptr) {
   const int q = threadIdx.x;
-  if (chain_pub && q < chain_words) {
+  if (chain_pub && q < chain_words && !published) {
     if (epoch) {
       constexpr int kKWords = static_cast<int>(sizeof(Consts) / 4);
       const uint32_t* dw = reinterpret_cast<const uint32_t*>(s_head);
@@ -895,13 +936,19 @@ __device__ __forceinline__ void store_update(EpisodeHead* H, const uint64_t* s_h
       chain_pub[q] = 0ull;
     }
   }
-  if (q < kStagedWords) reinterpret_cast<uint64_t*>(H)[q] = s_head[q];   // head, then StaleTraj
+  constexpr int kKQ = static_cast<int>(sizeof(Consts) / 8);
+  if (q < kStoredWords)   // head, then StaleTraj
+    reinterpret_cast<uint64_t*>(H)[q] =
+        (published && q < kKQ) ? reinterpret_cast<const uint64_t*>(pub)[q] : s_head[q];
   if (slot && q < kLogWords) reinterpret_cast<uint64_t*>(slot)[q] = s_log[q];
 }
 
 __device__ void episode_hook(const mpc_episode_config_t& c, const EpisodeHook& h,
                              const Winner& r, EpisodeHead& H, StaleTraj& st,
-                             mpc_episode_log_t& L, mpc_episode_log_t*& slot);
+                             mpc_episode_log_t& L, mpc_episode_log_t*& slot,
+                             const uint32_t* early = nullptr, bool* early_bad = nullptr);
+__device__ inline void episode_early_prepare(const mpc_episode_config_t& c, const EpisodeHead& S,
+                                             const StaleTraj& st, EarlyPub& E);
 
 // Block-record reduction + winner re-roll (+ episode update), run by every
 // thread of one block of NT threads.  SC1: the records were written by
@@ -959,6 +1006,16 @@ __device__ __forceinline__ void load8_rec_sc1_sbase(const Rec* base, const uint3
       : "memory");
 }
 
+// The end-of-step checks of a candidate next pose that episode_advance makes
+// after the events (none in the early publication's steps): the
+// run_math_model stuck break (:266-272) and the arrival (:542).
+__device__ __forceinline__ bool early_pose_ok(const mpc_episode_config_t& c, const EpisodeHead& H,
+                                              double x, double y) {
+  if (c.stop_rule == 1 && x == H.x && y == H.y && H.recursive >= 1) return false;
+  const double ex = H.x_t - x, ey = H.y_t - y;
+  return !(ex * ex + ey * ey <= c.eps);
+}
+
 // GEN (generated controls, k_rollout_generated): v / b are [n_part][MPC_MAX_STEPS]
 // — the controls of each rollout block's best candidate — instead of the
 // [n_steps][n_cand] candidate arrays; the winner's are those of its block.
@@ -979,8 +1036,18 @@ __device__ __forceinline__ void finalize_block(
   __shared__ mpc_episode_log_t* s_slot;
   __shared__ uint64_t s_key[NT / 64];
   __shared__ int64_t s_idx[NT / 64];
+  // the early publication (chained step's block 0, below)
+  constexpr int kKWords = static_cast<int>(sizeof(Consts) / 4);
+  __shared__ __attribute__((aligned(8))) uint32_t s_pub[64];
+  __shared__ double2 s_sc[4];
+  __shared__ int s_early;
   uint64_t k = ~0ull;
   int64_t i = INT64_MAX;
+  // wave 1's head words, loaded BEFORE its records so that both are in flight
+  // together (the block barrier after the reduction waits for the staging)
+  const bool stage = KDEV && hook.H && threadIdx.x >= 64 && threadIdx.x < 64 + kStagedWords;
+  const uint64_t head_word =
+      stage ? reinterpret_cast<const uint64_t*>(hook.H)[threadIdx.x - 64] : 0ull;
   if constexpr (SC1) {
     // n_part <= kMaxBlocks = 8 * NT: eight loads per thread, addresses of
     // out-of-range slots clamped to a valid record and their values ignored
@@ -1000,6 +1067,14 @@ __device__ __forceinline__ void finalize_block(
         k = r[q].x;
         i = static_cast<int64_t>(r[q].y);
       }
+  } else if (n_part <= NT) {
+    // at most one record per thread (a small launch, config B's 196): no
+    // compare chain over seven sentinel records on the selection's path
+    if (static_cast<int>(threadIdx.x) < n_part) {
+      const Rec r = part[threadIdx.x];
+      k = r.key;
+      i = r.idx;
+    }
   } else {
     // all of this thread's records are loaded before any is compared, so
     // the loads overlap (one memory round trip)
@@ -1017,9 +1092,13 @@ __device__ __forceinline__ void finalize_block(
         i = r[q].idx;
       }
   }
-  if (KDEV && hook.H && threadIdx.x >= 64 && threadIdx.x < 64 + kStagedWords)
-    s_head[threadIdx.x - 64] = reinterpret_cast<const uint64_t*>(hook.H)[threadIdx.x - 64];
-  wave_argmin(k, i);
+  if (stage) s_head[threadIdx.x - 64] = head_word;
+  // record indices are local candidate indices: below 2^31 for any row the
+  // candidate arrays can hold in practice -> three 32-bit DPP minima
+  if (!GEN && n_cand < (int64_t{1} << 31))
+    wave_argmin32(k, i);
+  else
+    wave_argmin(k, i);
   // Each wave's best candidate's controls, loaded while the waves' minima are
   // combined: the block's winner is one of them, so its re-roll starts
   // without a dependent load of its own (one memory round trip fewer on the
@@ -1064,21 +1143,122 @@ __device__ __forceinline__ void finalize_block(
     const int64_t col = k == ~0ull ? 0 : ((i / (kBlock * 2)) % n_part) * MPC_MAX_STEPS;
     emit_winner<INTEG, ROT>(K, v, b, 1, n_steps, k, col, index_base + i, incumbent, out, lds, &w);
   } else {
+    // A chained step's block 0: in the common step (no event, no end of the
+    // episode) the next step's published words follow from the new pose
+    // alone, so they go out before the rest of the update — the tile blocks
+    // waiting for them do not also wait for the log record, the stale
+    // trajectory, the event and restart logic and the head's stores.  What
+    // does not need the winner was formed by the previous update (the head's
+    // early_* fields); wave 3 lays out the words that carry over while wave 0
+    // forms the per-step factors, and wave 1 evaluates sin / cos of the
+    // winner's layer headings (the pass's own sums, in its order) during lane
+    // 0's serial pass.
+    const EpisodeHead& Hs = *reinterpret_cast<const EpisodeHead*>(s_head);
+    const EarlyPub& Es = *reinterpret_cast<const EarlyPub*>(&s_head[kStoredWords]);
+    const bool early_on = KDEV && hook.H && hook.publish_epoch;
+    auto side_a = [&]() {
+      const int q = threadIdx.x - 192;
+      if (!early_on || q < 0 || q >= 64) return;
+      constexpr int kH = static_cast<int>(offsetof(Consts, h) / 4);
+      constexpr int kHl = static_cast<int>(offsetof(Consts, hlgth) / 4);
+      static_assert(kHl == kH + 2, "h, hlgth adjacent");
+      const uint32_t* kw = reinterpret_cast<const uint32_t*>(s_head);   // Hs.K's dwords
+      const uint32_t* ew = reinterpret_cast<const uint32_t*>(&Es.t);   // t, h, hl
+      if (q < kKWords)
+        s_pub[q] = (q >= kH && q < kH + 4) ? ew[2 + (q - kH)] : kw[q];
+      else if (q < kKWords + 2)
+        s_pub[q] = ew[q - kKWords];
+    };
+    auto side_b = [&](bool fast) {
+      const int q = threadIdx.x;
+      if (early_on && q >= 64 && q < 64 + 3) {
+        const int last = n_steps - 1, jj = q - 64 < last ? q - 64 : last;
+        double ph;
+        if (fast) {   // emit_winner's fast pass: K.phi + dphi_0 + ... in step order
+          ph = K.phi;
+          for (int st = 0; st <= jj; ++st) ph = ph + lds->dphi[st];
+        } else {
+          ph = lds->phi[jj];
+        }
+        double sn, cs;
+        trig::sincos_fast(ph, &sn, &cs);
+        s_sc[q - 64] = make_double2(sn, cs);
+      }
+    };
     emit_winner<INTEG, ROT>(K, v, b, n_cand, n_steps, k, i, index_base + i, incumbent, out, lds,
-                            &w, s_pv, s_pb, KDEV && hook.H);
+                            &w, s_pv, s_pb, KDEV && hook.H, side_a, side_b);
   }
   if (KDEV && hook.H) {
-    if (threadIdx.x == 0) {   // emit_winner ended with a barrier
-      EpisodeHead H;
-      __builtin_memcpy(&H, s_head, sizeof(EpisodeHead));
-      episode_hook(ecfg, hook, w, H, *reinterpret_cast<StaleTraj*>(&s_head[kHeadWords]), s_log,
-                   s_slot);
-      __builtin_memcpy(s_head, &H, sizeof(EpisodeHead));
+    // (the early publication, see emit_winner's side work above: thread 0
+    // picks the pose and writes what changes; wave 0 publishes)
+    if (hook.publish_epoch && threadIdx.x < 64) {   // (emit_winner ended with a barrier)
+      const EpisodeHead& Hs = *reinterpret_cast<const EpisodeHead*>(s_head);
+      const EarlyPub& Es = *reinterpret_cast<const EarlyPub*>(&s_head[kStoredWords]);
+      const int q = threadIdx.x;
+      if (q == 0) {
+        const int pre = Es.step == Hs.step ? Es.k : -1;
+        int j = -1;
+        double x = 0.0, y = 0.0, ph = 0.0;
+        if (pre >= 0) {
+          if (w.found) {   // winner layer min(k, N-1): episode_advance's st.ot[k]
+            const int last = w.n_steps - 1, jj = pre < last ? pre : last;
+            x = tr_at(w, jj, 0);
+            y = tr_at(w, jj, 1);
+            ph = tr_at(w, jj, 2);
+            if (early_pose_ok(ecfg, Hs, x, y)) j = jj;
+          } else if (Es.alt) {
+            j = 3;
+            x = Es.x;
+            y = Es.y;
+            ph = Es.ph;
+            double sn, cs;
+            trig::sincos_fast(ph, &sn, &cs);
+            s_sc[3] = make_double2(sn, cs);
+          }
+        }
+        if (j >= 0) {
+          Consts& Kp = *reinterpret_cast<Consts*>(s_pub);
+          Kp.x = x;
+          Kp.y = y;
+          Kp.phi = ph;
+          Kp.s0 = s_sc[j].x;
+          Kp.c0 = s_sc[j].y;
+        }
+        s_early = j >= 0 ? 1 : 0;
+      }
+      // lane 0's LDS stores, then wave 0's reads (one wave: no block barrier)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (s_early && q < hook.chain_pub_words)
+        __hip_atomic_store(&hook.chain_pub[q],
+                           (static_cast<uint64_t>(s_pub[q]) << 32) | hook.publish_epoch,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const bool early = hook.publish_epoch && s_early;   // (uniform)
+    if (threadIdx.x == 0) {
+      // on the LDS copy itself: the update touches a few of its words, and a
+      // copy into registers and back costs more than it saves; after an early
+      // publication the constants are left as published
+      bool bad = false;
+      episode_hook(ecfg, hook, w, *reinterpret_cast<EpisodeHead*>(s_head),
+                   *reinterpret_cast<StaleTraj*>(&s_head[kHeadWords]), s_log, s_slot,
+                   early ? s_pub : nullptr, &bad);
+      if (bad && hook.chain_error) *hook.chain_error = 6u;
     }
     __syncthreads();
-    // the head and the log record back to HBM, the chain tags cleared
+    if (hook.publish_epoch && threadIdx.x == 64) {
+      // the next step's early-publication inputs, beside the head's stores
+      // (an EarlyPub follows the stale trajectory in the state)
+      EarlyPub E;
+      episode_early_prepare(ecfg, *reinterpret_cast<const EpisodeHead*>(s_head),
+                            *reinterpret_cast<const StaleTraj*>(&s_head[kHeadWords]), E);
+      *reinterpret_cast<EarlyPub*>(reinterpret_cast<uint64_t*>(hook.H) + kStoredWords) = E;
+    }
+    // the head and the log record back to HBM, the chain tags cleared (or the
+    // next step's constants published, unless they already are)
     store_update(hook.H, s_head, s_slot, reinterpret_cast<const uint64_t*>(&s_log),
-                 hook.chain_pub, hook.chain_pub_words, hook.publish_epoch);
+                 hook.chain_pub, hook.chain_pub_words, hook.publish_epoch, early, s_pub);
     // the record's remaining trajectory, off the update's critical path
     emit_winner_tail<INTEG, ROT>(K, n_steps, lds, out);
   }

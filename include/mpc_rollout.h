@@ -433,13 +433,14 @@ int mpc_episode_exchange_flush(const mpc_episode_config_t* cfg, void* state, int
  *   (ws / ws_prev alternated, the previous step's controls v_prev / beta_prev)
  *   whose block 0 reduces the previous launch's block records into this
  *   rank's candidate, stores it into slot prev_epoch & 1 of every rank's
- *   mailbox (then the tags), waits (bounded, ~1 s; chain error 5) for the
+ *   mailbox (then the tags), waits (bounded, 2 s; chain error 5) for the
  *   world candidates in its own mailbox, selects the (cost, global index)
  *   minimum, re-rolls it into out_prev (the global winner, on every rank),
  *   updates the episode and publishes this step's constants; the tile blocks
  *   meanwhile roll out this rank's shard (index_base).
- * Consecutive epochs must differ in parity (the two slots alternate); every
- * rank runs the same sequence of epochs.  The chain ends with
+ * Consecutive epochs must differ in parity; the mailbox slot is chosen on the
+ * device by the episode's count of P2P completions; every rank runs the same
+ * sequence of epochs.  The chain ends with
  * mpc_episode_p2p_flush (the last step's controls and workspace).  No host
  * step and no collective between launches: plain kernels on one stream,
  * graph-capturable (end a captured sequence with the flush, as above).
@@ -514,7 +515,10 @@ int mpc_episode_generate_step(const mpc_episode_config_t* cfg, void* state, int6
  * (the step was not completed: the episode kept its pose); 5 = a P2P exchange
  * step's wait for the ranks' candidates in its mailbox timed out (a peer did
  * not run the same step; the step was not completed, and the later steps of
- * the episode fail fast instead of waiting again).
+ * the episode fail fast instead of waiting again); 6 = a one-GPU chained
+ * step's early publication of the next constants (formed from the new pose
+ * before the rest of the update, in a step without event or restart)
+ * differed from the update's own (a self-check: never expected).
  * The waits are bounded on the GPU's wall clock: 0.2 s for a one-GPU chained
  * launch's tiles; 2 s for block 0's wait for peers or a collective (4, 5); 3 s
  * for the tiles of an exchange / P2P launch, so a late peer is never scored as

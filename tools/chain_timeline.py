@@ -3,7 +3,7 @@ the library with s_memrealtime (100 MHz) stamps patched into a copy of the
 sources (the shipped sources carry none), then one chained step among
 back-to-back ones, decoded per phase.
 
-    python tools/chain_timeline.py build            # -> tools/var_timeline.so (CPU)
+    python tools/chain_timeline.py build            # -> tools/tl_variant.so (CPU)
     python tools/chain_timeline.py run N_CAND N [p2p]   # on the GPU box (p2p: the
                                                     # one-rank P2P exchange form)
 
@@ -22,10 +22,11 @@ import sys
 import tempfile
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VAR = os.path.join(REPO, "tools", "var_timeline.so")
+VAR = os.path.join(REPO, "tools", "tl_variant.so")   # git-ignored; delete after use (every gpurun call ships it)
 NB = 2048 + 1
 B0 = ["entry", "records", "wave argmin", "block winner", "controls in LDS", "re-roll",
-      "advance", "update", "published", "adv-entry", "finishing", "pre-prepare", "prepared"]
+      "advance", "update", "published", "adv-entry", "finishing", "pre-prepare", "prepared",
+      "early pub", "tail done", "t64 early prep"]
 B0_BASE = 8 * NB   # block 0's stamps follow the tiles' (8 per block)
 TILE = ["entry", "DMAs issued", "final consts", "record stored"]
 
@@ -52,22 +53,25 @@ def build():
     b0 = lambda q: f"if (blockIdx.x == 0 && threadIdx.x == 0) {st(B0_BASE + q)};"   # noqa: E731
     patch(os.path.join(cs, "mpc_kernels.h"), [
         ("struct Rec {\n", f"__device__ uint64_t g_tl[8 * {NB} + 16];\n\nstruct Rec {{\n"),
-        ("  if (KDEV && hook.H && threadIdx.x >= 64 && threadIdx.x < 64 + kStagedWords)\n"
-         "    s_head[threadIdx.x - 64]",
+        ("  if (stage) s_head[threadIdx.x - 64] = head_word;\n",
          f"  {b0(1)}\n"
-         "  if (KDEV && hook.H && threadIdx.x >= 64 && threadIdx.x < 64 + kStagedWords)\n"
-         "    s_head[threadIdx.x - 64]"),
+         "  if (stage) s_head[threadIdx.x - 64] = head_word;\n"),
         ("  wave_argmin(k, i);\n  // Each wave's best", f"  wave_argmin(k, i);\n  {b0(2)}\n  // Each wave's best"),
         ("  int wbest = 0;\n", f"  {b0(3)}\n  int wbest = 0;\n"),
-        ("  if (KDEV && hook.H) {\n    if (threadIdx.x == 0) {   // emit_winner ended with a barrier\n",
-         f"  {b0(5)}\n  if (KDEV && hook.H) {{\n    if (threadIdx.x == 0) {{   // emit_winner ended with a barrier\n"),
-        ("      __builtin_memcpy(s_head, &H, sizeof(EpisodeHead));\n    }\n    __syncthreads();\n"
-         "    // the head and the log record back to HBM, the chain tags cleared\n",
-         f"      __builtin_memcpy(s_head, &H, sizeof(EpisodeHead));\n      {b0(7)}\n    }}\n"
-         "    __syncthreads();\n"
-         "    // the head and the log record back to HBM, the chain tags cleared\n"),
-        ("                 hook.chain_pub, hook.chain_pub_words, hook.publish_epoch);\n",
-         "                 hook.chain_pub, hook.chain_pub_words, hook.publish_epoch);\n"
+        ("  if (KDEV && hook.H) {\n    // (the early publication,",
+         f"  {b0(5)}\n  if (KDEV && hook.H) {{\n    // (the early publication,"),
+        ("__HIP_MEMORY_SCOPE_AGENT);\n    }\n    const bool early = hook.publish_epoch && s_early;",
+         f"__HIP_MEMORY_SCOPE_AGENT);\n      {b0(13)}\n    }}\n"
+         "    const bool early = hook.publish_epoch && s_early;"),
+        ("                   early ? s_pub : nullptr, &bad);\n",
+         f"                   early ? s_pub : nullptr, &bad);\n      {b0(7)}\n"),
+        ("      *reinterpret_cast<EarlyPub*>(reinterpret_cast<uint64_t*>(hook.H) + kStoredWords) = E;\n",
+         "      *reinterpret_cast<EarlyPub*>(reinterpret_cast<uint64_t*>(hook.H) + kStoredWords) = E;\n"
+         f"      if (blockIdx.x == 0) {STAMP.format(slot=B0_BASE + 15)};\n"),
+        ("    emit_winner_tail<INTEG, ROT>(K, n_steps, lds, out);\n  }\n}\n",
+         f"    emit_winner_tail<INTEG, ROT>(K, n_steps, lds, out);\n    {b0(14)}\n  }}\n}}\n"),
+        ("                 hook.chain_pub, hook.chain_pub_words, hook.publish_epoch, early, s_pub);\n",
+         "                 hook.chain_pub, hook.chain_pub_words, hook.publish_epoch, early, s_pub);\n"
          f"    {b0(8)}\n"),
         ("  __syncthreads();\n  // Regular rotation-mode winner",
          f"  __syncthreads();\n  {b0(4)}\n  // Regular rotation-mode winner"),
@@ -89,8 +93,9 @@ def build():
          f"  {b0(9)}\n  EpisodeHead* S = &H;\n  S->steps_for_slowing -= 1;\n"),
         ("  const double x_prev = S->x, y_prev = S->y;   // x_previous",
          f"  {b0(10)}\n  const double x_prev = S->x, y_prev = S->y;   // x_previous"),
-        ("    episode_restart(c, *S);\n  }\n  episode_prepare(c, *S);\n}\n",
-         f"    episode_restart(c, *S);\n  }}\n  {b0(11)}\n  episode_prepare(c, *S);\n  {b0(12)}\n}}\n"),
+        ("  if (early && (ended ||", f"  {b0(11)}\n  if (early && (ended ||"),
+        ("  } else {\n    episode_prepare(c, *S);\n  }\n}\n",
+         f"  }} else {{\n    episode_prepare(c, *S);\n  }}\n  {b0(12)}\n}}\n"),
         ("  L.status = status;\n  if (ended) {\n",
          f"  L.status = status;\n  {b0(6)}\n  if (ended) {{\n"),
         ("  if (blockIdx.x == 0) {\n    if (has_prev) {\n",
