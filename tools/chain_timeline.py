@@ -26,7 +26,7 @@ VAR = os.path.join(REPO, "tools", "tl_variant.so")   # git-ignored; delete after
 NB = 2048 + 1
 B0 = ["entry", "records", "wave argmin", "block winner", "controls in LDS", "re-roll",
       "advance", "update", "published", "adv-entry", "finishing", "pre-prepare", "prepared",
-      "early pub", "tail done", "t64 early prep"]
+      "early pub", "tail done", "t64 early prep", "ew bcast", "ew phase1"]
 B0_BASE = 8 * NB   # block 0's stamps follow the tiles' (8 per block)
 TILE = ["entry", "DMAs issued", "final consts", "record stored"]
 
@@ -52,7 +52,11 @@ def build():
     st = lambda slot: STAMP.format(slot=slot)   # noqa: E731
     b0 = lambda q: f"if (blockIdx.x == 0 && threadIdx.x == 0) {st(B0_BASE + q)};"   # noqa: E731
     patch(os.path.join(cs, "mpc_kernels.h"), [
-        ("struct Rec {\n", f"__device__ uint64_t g_tl[8 * {NB} + 16];\n\nstruct Rec {{\n"),
+        ("  __syncthreads();\n  key = s_key;\n", f"  __syncthreads();\n  {b0(16)}\n  key = s_key;\n"),
+        ("  side_a();\n", f"  {b0(17)}\n  side_a();\n"),
+    ])
+    patch(os.path.join(cs, "mpc_kernels.h"), [
+        ("struct Rec {\n", f"__device__ uint64_t g_tl[8 * {NB} + 32];\n\nstruct Rec {{\n"),
         ("  if (stage) s_head[threadIdx.x - 64] = head_word;\n",
          f"  {b0(1)}\n"
          "  if (stage) s_head[threadIdx.x - 64] = head_word;\n"),
@@ -147,7 +151,7 @@ def run(n, ns, mode="chain"):
     L = native.lib()
     L.mpc_debug_timeline.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     nb = (n + 511) // 512 + 1
-    buf = (ctypes.c_uint64 * (8 * NB + 16))()
+    buf = (ctypes.c_uint64 * (8 * NB + 32))()
     rows = []
     for rep in range(5):
         for i in range(300):
