@@ -1188,9 +1188,9 @@ def traffic_summary(traffic_json, kernel, bytes_launch, layout="soa"):
 # SQ_INSTS_VALU) of each kernel at the size it was measured on:
 # (kernel, integrator) -> (summary, candidates, horizon) — config C, or the
 # S1 = 451 full tree of config F (candidates = leaves)
-VALU_JSON = {("k_episode_chain", "rect+cum"): ("r04_final/valu/chain.json", 1_000_000, 10),
-             ("k_rollout_argmin_stream", "qk21"): ("r04_final/valu/qk21.json", 1_000_000, 10),
-             ("k_rollout_generated", "rect+cum"): ("r04_final/valu/gen.json", 1_000_000, 10),
+VALU_JSON = {("k_episode_chain", "rect+cum"): ("r05/valu/chain.json", 1_000_000, 10),
+             ("k_rollout_argmin_stream", "qk21"): ("r05/valu/qk21.json", 1_000_000, 10),
+             ("k_rollout_generated", "rect+cum"): ("r05/valu/gen.json", 1_000_000, 10),
              ("k_ft_leaves", "rect+rot"): ("r05/valu/ft.json", 451 ** 3, 3),
              # the device-resident episode drivers: the whole run is ONE launch;
              # keyed (episodes, max_calls) of workloads R and G as the bench runs them
