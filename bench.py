@@ -713,7 +713,8 @@ def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
         out["roofline"]["stream_ceiling_GBs"] = ceil
         out["roofline"]["stream_ceiling_ms"] = ceil_ms
         out["roofline"]["frac_of_stream_ceiling"] = achieved / ceil
-        out["roofline"]["valu"] = valu_share(args.traffic_json, kernel, bytes_launch, kern_ms)
+        out["roofline"]["valu"] = valu_share(args.traffic_json, kernel, bytes_launch, kern_ms,
+                                             out["roofline"].get("layout", "soa"))
     return out, ep, pool
 
 
@@ -872,12 +873,12 @@ def host_latency_pass(ep, pool, n=200):
     return out
 
 
-def valu_share(traffic_json, kernel, bytes_launch, kern_ms):
+def valu_share(traffic_json, kernel, bytes_launch, kern_ms, layout="soa"):
     """VALU wave-instructions per launch (SQ_INSTS_VALU, PMC) and the share of
     the fp64 issue rate they take: 4 cycles per wave-instruction on each of the
     1024 SIMDs at 2.4 GHz (78.6 TFLOP/s of fp64 FMA); integer and fp32 VALU
     instructions are counted as fp64 ones, so the share is an upper bound."""
-    t, path = traffic_summary(traffic_json, kernel, bytes_launch)
+    t, path = traffic_summary(traffic_json, kernel, bytes_launch, layout)
     insts = t.get("counters_median_per_launch", {}).get("SQ_INSTS_VALU") if t else None
     if insts is None:
         return None
