@@ -632,16 +632,19 @@ __device__ __forceinline__ EmitLds* ring_lds() {
 struct NoSide {
   __device__ void operator()() const {}
   __device__ void operator()(bool) const {}
+  __device__ void operator()(int, double, double, double) const {}
 };
 
-template <int INTEG, int ROT, class SideA = NoSide, class SideB = NoSide>
+// on_layer(st, x, y, phi): lane 0, in the serial pass, as each of the first
+// three layer states is formed.
+template <int INTEG, int ROT, class SideA = NoSide, class SideB = NoSide, class OnLayer = NoSide>
 __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
                             const double* __restrict__ b, int64_t ld, int n_steps, uint64_t key,
                             int64_t col, int64_t reported_index, double incumbent,
                             mpc_result_t* __restrict__ out, EmitLds* lds, Winner* win = nullptr,
                             const double* pre_v = nullptr, const double* pre_b = nullptr,
                             bool defer_tail = false, const SideA& side_a = SideA{},
-                            const SideB& side_b = SideB{}) {
+                            const SideB& side_b = SideB{}, const OnLayer& on_layer = OnLayer{}) {
   double* s_v = lds->v;
   double* s_dphi = lds->dphi;
   double* s_phi = lds->phi;
@@ -795,6 +798,7 @@ __device__ void emit_winner(const Consts& K, const double* __restrict__ v,
           win->tr[st][1] = py;
           win->tr[st][2] = ph;
         }
+        if (st < 3) on_layer(st, px, py, ph);
       }
       if (n_run < n_steps) {
         lds->tail[0] = x;
@@ -1039,8 +1043,8 @@ __device__ __forceinline__ void finalize_block(
   // the early publication (chained step's block 0, below)
   constexpr int kKWords = static_cast<int>(sizeof(Consts) / 4);
   __shared__ __attribute__((aligned(8))) uint32_t s_pub[64];
-  __shared__ double2 s_sc[4];
-  __shared__ int s_early;
+  __shared__ double2 s_sc[3];
+  __shared__ int s_early, s_pose, s_sc_ready;
   uint64_t k = ~0ull;
   int64_t i = INT64_MAX;
   // wave 1's head words, loaded BEFORE its records so that both are in flight
@@ -1169,6 +1173,31 @@ __device__ __forceinline__ void finalize_block(
       else if (q < kKWords + 2)
         s_pub[q] = ew[q - kKWords];
     };
+    // The pick: the winner's layer jj = min(k, N-1) as lane 0 forms it in the
+    // serial pass (on_layer: the end-of-step checks, the pose into s_pub,
+    // s_pose = 1 publish / 2 not), or the no-winner pose (decided by wave 3
+    // alone); wave 3 then adds sin / cos and publishes — while lane 0 goes on
+    // with the remaining layers.
+    const bool can_early =
+        early_on && Es.step == Hs.step && Es.k >= 0;   // (uniform: LDS words, all threads)
+    const bool valid_w = k != ~0ull;
+    const bool found_w = valid_w && key_cost(k) < incumbent;   // emit_winner's `found`
+    const int jj_w = can_early ? (Es.k < n_steps - 1 ? Es.k : n_steps - 1) : -1;
+    if (threadIdx.x == 0) {   // (LDS starts undefined; read only after emit_winner's barriers)
+      s_pose = 0;
+      s_sc_ready = 0;
+    }
+    auto on_layer = [&](int st, double x, double y, double ph) {
+      if (!can_early || !found_w || st != jj_w) return;
+      const bool ok = early_pose_ok(ecfg, Hs, x, y);
+      if (ok) {
+        Consts& Kp = *reinterpret_cast<Consts*>(s_pub);
+        Kp.x = x;
+        Kp.y = y;
+        Kp.phi = ph;
+      }
+      __hip_atomic_store(&s_pose, ok ? 1 : 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
     auto side_b = [&](bool fast) {
       const int q = threadIdx.x;
       if (early_on && q >= 64 && q < 64 + 3) {
@@ -1183,58 +1212,60 @@ __device__ __forceinline__ void finalize_block(
         double sn, cs;
         trig::sincos_fast(ph, &sn, &cs);
         s_sc[q - 64] = make_double2(sn, cs);
+        if (q == 64)   // (the wave's three LDS stores are in order before it)
+          __hip_atomic_store(&s_sc_ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      if (early_on && q >= 192 && q < 256) {   // wave 3: the pick's last part, the publication
+        if (q == 192) {
+          int pub = 0;
+          if (can_early) {
+            Consts& Kp = *reinterpret_cast<Consts*>(s_pub);
+            if (!found_w) {   // the no-winner pose: the stale layer k, or the pose
+              if (Es.alt) {
+                double sn, cs;
+                trig::sincos_fast(Es.ph, &sn, &cs);
+                Kp.x = Es.x;
+                Kp.y = Es.y;
+                Kp.phi = Es.ph;
+                Kp.s0 = sn;
+                Kp.c0 = cs;
+                pub = 1;
+              }
+            } else {
+              // lane 0's pose and wave 1's sin / cos (bounded waits: an
+              // unanswered one only forgoes the early publication)
+              int pose = 0, sc = 0;
+              for (uint32_t it = 0; it < (1u << 22) && (pose == 0 || sc == 0); ++it) {
+                pose = __hip_atomic_load(&s_pose, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                sc = __hip_atomic_load(&s_sc_ready, __ATOMIC_ACQUIRE,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (pose == 2) break;
+                if (pose == 0 || sc == 0) __builtin_amdgcn_s_sleep(1);
+              }
+              if (pose == 1 && sc == 1) {
+                Kp.s0 = s_sc[jj_w].x;
+                Kp.c0 = s_sc[jj_w].y;
+                pub = 1;
+              }
+            }
+          }
+          s_early = pub;
+        }
+        // thread 192's LDS stores, then wave 3's reads (one wave)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int w3 = q - 192;
+        if (s_early && w3 < hook.chain_pub_words)
+          __hip_atomic_store(&hook.chain_pub[w3],
+                             (static_cast<uint64_t>(s_pub[w3]) << 32) | hook.publish_epoch,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     };
     emit_winner<INTEG, ROT>(K, v, b, n_cand, n_steps, k, i, index_base + i, incumbent, out, lds,
-                            &w, s_pv, s_pb, KDEV && hook.H, side_a, side_b);
+                            &w, s_pv, s_pb, KDEV && hook.H, side_a, side_b, on_layer);
   }
   if (KDEV && hook.H) {
-    // (the early publication, see emit_winner's side work above: thread 0
-    // picks the pose and writes what changes; wave 0 publishes)
-    if (hook.publish_epoch && threadIdx.x < 64) {   // (emit_winner ended with a barrier)
-      const EpisodeHead& Hs = *reinterpret_cast<const EpisodeHead*>(s_head);
-      const EarlyPub& Es = *reinterpret_cast<const EarlyPub*>(&s_head[kStoredWords]);
-      const int q = threadIdx.x;
-      if (q == 0) {
-        const int pre = Es.step == Hs.step ? Es.k : -1;
-        int j = -1;
-        double x = 0.0, y = 0.0, ph = 0.0;
-        if (pre >= 0) {
-          if (w.found) {   // winner layer min(k, N-1): episode_advance's st.ot[k]
-            const int last = w.n_steps - 1, jj = pre < last ? pre : last;
-            x = tr_at(w, jj, 0);
-            y = tr_at(w, jj, 1);
-            ph = tr_at(w, jj, 2);
-            if (early_pose_ok(ecfg, Hs, x, y)) j = jj;
-          } else if (Es.alt) {
-            j = 3;
-            x = Es.x;
-            y = Es.y;
-            ph = Es.ph;
-            double sn, cs;
-            trig::sincos_fast(ph, &sn, &cs);
-            s_sc[3] = make_double2(sn, cs);
-          }
-        }
-        if (j >= 0) {
-          Consts& Kp = *reinterpret_cast<Consts*>(s_pub);
-          Kp.x = x;
-          Kp.y = y;
-          Kp.phi = ph;
-          Kp.s0 = s_sc[j].x;
-          Kp.c0 = s_sc[j].y;
-        }
-        s_early = j >= 0 ? 1 : 0;
-      }
-      // lane 0's LDS stores, then wave 0's reads (one wave: no block barrier)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (s_early && q < hook.chain_pub_words)
-        __hip_atomic_store(&hook.chain_pub[q],
-                           (static_cast<uint64_t>(s_pub[q]) << 32) | hook.publish_epoch,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     const bool early = hook.publish_epoch && s_early;   // (uniform)
     if (threadIdx.x == 0) {
       // on the LDS copy itself: the update touches a few of its words, and a

@@ -26,7 +26,7 @@ VAR = os.path.join(REPO, "tools", "tl_variant.so")   # git-ignored; delete after
 NB = 2048 + 1
 B0 = ["entry", "records", "wave argmin", "block winner", "controls in LDS", "re-roll",
       "advance", "update", "published", "adv-entry", "finishing", "pre-prepare", "prepared",
-      "early pub", "tail done", "t64 early prep", "ew bcast", "ew phase1"]
+      "early pub", "tail done", "t64 early prep", "ew bcast", "ew phase1", "w1 sincos", "l0 pose"]
 B0_BASE = 8 * NB   # block 0's stamps follow the tiles' (8 per block)
 TILE = ["entry", "DMAs issued", "final consts", "record stored"]
 
@@ -52,6 +52,14 @@ def build():
     st = lambda slot: STAMP.format(slot=slot)   # noqa: E731
     b0 = lambda q: f"if (blockIdx.x == 0 && threadIdx.x == 0) {st(B0_BASE + q)};"   # noqa: E731
     patch(os.path.join(cs, "mpc_kernels.h"), [
+        ("          __hip_atomic_store(&s_sc_ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);\n",
+         "          __hip_atomic_store(&s_sc_ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
+         f"        if (blockIdx.x == 0 && q == 64) {STAMP.format(slot=B0_BASE + 18)};\n"),
+        ("      __hip_atomic_store(&s_pose, ok ? 1 : 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);\n",
+         "      __hip_atomic_store(&s_pose, ok ? 1 : 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
+         f"      if (blockIdx.x == 0) {STAMP.format(slot=B0_BASE + 19)};\n"),
+    ])
+    patch(os.path.join(cs, "mpc_kernels.h"), [
         ("  __syncthreads();\n  key = s_key;\n", f"  __syncthreads();\n  {b0(16)}\n  key = s_key;\n"),
         ("  side_a();\n", f"  {b0(17)}\n  side_a();\n"),
     ])
@@ -62,11 +70,12 @@ def build():
          "  if (stage) s_head[threadIdx.x - 64] = head_word;\n"),
         ("  wave_argmin(k, i);\n  // Each wave's best", f"  wave_argmin(k, i);\n  {b0(2)}\n  // Each wave's best"),
         ("  int wbest = 0;\n", f"  {b0(3)}\n  int wbest = 0;\n"),
-        ("  if (KDEV && hook.H) {\n    // (the early publication,",
-         f"  {b0(5)}\n  if (KDEV && hook.H) {{\n    // (the early publication,"),
-        ("__HIP_MEMORY_SCOPE_AGENT);\n    }\n    const bool early = hook.publish_epoch && s_early;",
-         f"__HIP_MEMORY_SCOPE_AGENT);\n      {b0(13)}\n    }}\n"
-         "    const bool early = hook.publish_epoch && s_early;"),
+        ("  if (KDEV && hook.H) {\n    const bool early = hook.publish_epoch && s_early;",
+         f"  {b0(5)}\n  if (KDEV && hook.H) {{\n    const bool early = hook.publish_epoch && s_early;"),
+        ("                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n      }\n    };\n",
+         "                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+         f"        if (blockIdx.x == 0 && threadIdx.x == 192) {STAMP.format(slot=B0_BASE + 13)};\n"
+         "      }\n    };\n"),
         ("                   early ? s_pub : nullptr, &bad);\n",
          f"                   early ? s_pub : nullptr, &bad);\n      {b0(7)}\n"),
         ("      *reinterpret_cast<EarlyPub*>(reinterpret_cast<uint64_t*>(hook.H) + kStoredWords) = E;\n",
