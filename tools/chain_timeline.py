@@ -28,7 +28,7 @@ B0 = ["entry", "records", "wave argmin", "block winner", "controls in LDS", "re-
       "advance", "update", "published", "adv-entry", "finishing", "pre-prepare", "prepared",
       "early pub", "tail done", "t64 early prep", "ew bcast", "ew phase1", "w1 sincos", "l0 pose"]
 B0_BASE = 8 * NB   # block 0's stamps follow the tiles' (8 per block)
-TILE = ["entry", "DMAs issued", "final consts", "record stored"]
+TILE = ["entry", "DMAs issued", "final consts", "record stored", "costs done", "argmin done"]
 
 STAMP = "__hip_atomic_store(&g_tl[{slot}], __builtin_amdgcn_s_memrealtime(), " \
         "__ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)"
@@ -90,6 +90,10 @@ def build():
          f"  __syncthreads();\n  {b0(4)}\n  // Regular rotation-mode winner"),
     ])
     t = lambda q: f"if (threadIdx.x == 0) {STAMP.format(slot=f'8 * blockIdx.x + {q}')};"   # noqa: E731
+    patch(os.path.join(cs, "mpc_episode.h"), [
+        ("  block_argmin<true>(best_k, best_i);   // (indices < n_cand < 2^31)\n",
+         f"  {t(4)}\n  block_argmin<true>(best_k, best_i);   // (indices < n_cand < 2^31)\n  {t(5)}\n"),
+    ])
     patch(os.path.join(cs, "mpc_episode.h"), [
         # P2P block 0 (p2p_complete): candidate from the records, posted, the
         # world's gathered; published (advance_from_candidates' store_update)
