@@ -42,6 +42,8 @@ CHAIN_ERRORS = {
        "(the collective could not run beside the launch: the step was not completed)",
     5: "a P2P exchange launch's block 0 timed out waiting for the ranks' candidates in its "
        "mailbox (a peer did not run the same step: the step was not completed)",
+    6: "a one-GPU chained step's early publication of the next step's constants disagreed "
+       "with its update (a self-check: never expected)",
 }
 
 
