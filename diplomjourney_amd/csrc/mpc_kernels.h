@@ -1209,11 +1209,18 @@ __device__ __forceinline__ void finalize_block(
         } else {
           ph = lds->phi[jj];
         }
-        double sn, cs;
-        trig::sincos_fast(ph, &sn, &cs);
+        // sincos_fast's own core (the same bits) on its range; beyond it (a
+        // heading of more than 2^19 pi / 2, never in practice) no early
+        // publication — the large reduction's code would cost the kernel
+        // scratch memory
+        double sn = 0.0, cs = 0.0;
+        const bool in = fabs(ph) <= trig::kFastMax;
+        if (in) trig::sincos_core(ph, &sn, &cs);
         s_sc[q - 64] = make_double2(sn, cs);
+        const bool all_in = __ballot(!in) == 0;
         if (q == 64)   // (the wave's three LDS stores are in order before it)
-          __hip_atomic_store(&s_sc_ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_store(&s_sc_ready, all_in ? 1 : 2, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       if (early_on && q >= 192 && q < 256) {   // wave 3: the pick's last part, the publication
         if (q == 192) {
@@ -1221,9 +1228,9 @@ __device__ __forceinline__ void finalize_block(
           if (can_early) {
             Consts& Kp = *reinterpret_cast<Consts*>(s_pub);
             if (!found_w) {   // the no-winner pose: the stale layer k, or the pose
-              if (Es.alt) {
+              if (Es.alt && fabs(Es.ph) <= trig::kFastMax) {
                 double sn, cs;
-                trig::sincos_fast(Es.ph, &sn, &cs);
+                trig::sincos_core(Es.ph, &sn, &cs);   // (= sincos_fast on its range)
                 Kp.x = Es.x;
                 Kp.y = Es.y;
                 Kp.phi = Es.ph;
@@ -1239,7 +1246,7 @@ __device__ __forceinline__ void finalize_block(
                 pose = __hip_atomic_load(&s_pose, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 sc = __hip_atomic_load(&s_sc_ready, __ATOMIC_ACQUIRE,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (pose == 2) break;
+                if (pose == 2 || sc == 2) break;
                 if (pose == 0 || sc == 0) __builtin_amdgcn_s_sleep(1);
               }
               if (pose == 1 && sc == 1) {

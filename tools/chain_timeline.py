@@ -52,9 +52,10 @@ def build():
     st = lambda slot: STAMP.format(slot=slot)   # noqa: E731
     b0 = lambda q: f"if (blockIdx.x == 0 && threadIdx.x == 0) {st(B0_BASE + q)};"   # noqa: E731
     patch(os.path.join(cs, "mpc_kernels.h"), [
-        ("          __hip_atomic_store(&s_sc_ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);\n",
-         "          __hip_atomic_store(&s_sc_ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
-         f"        if (blockIdx.x == 0 && q == 64) {STAMP.format(slot=B0_BASE + 18)};\n"),
+        ("                             __HIP_MEMORY_SCOPE_WORKGROUP);\n      }\n      if (early_on && q >= 192",
+         "                             __HIP_MEMORY_SCOPE_WORKGROUP);\n"
+         f"        if (blockIdx.x == 0 && q == 64) {STAMP.format(slot=B0_BASE + 18)};\n"
+         "      }\n      if (early_on && q >= 192"),
         ("      __hip_atomic_store(&s_pose, ok ? 1 : 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);\n",
          "      __hip_atomic_store(&s_pose, ok ? 1 : 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
          f"      if (blockIdx.x == 0) {STAMP.format(slot=B0_BASE + 19)};\n"),
