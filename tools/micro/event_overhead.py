@@ -70,7 +70,25 @@ def main():
             dev["in_graph"].append(ei0.elapsed_time(ei1) * 1e3 / K)
         except Exception as e:   # noqa: BLE001
             dev["in_graph"].append(float("nan"))
+    # the bench's sequence: ~15 warm replays, ONE sync (the host waits ~10 ms),
+    # then the timed replay — with and without a host spin before it
+    for mode in ("bench", "bench+spin", "bench", "bench+spin", "bench", "bench+spin",
+                 "bench", "bench+spin"):
+        for _ in range(15):
+            g.replay()
+        torch.cuda.synchronize()
+        if mode.endswith("spin"):
+            t_end = time.perf_counter() + 0.003
+            while time.perf_counter() < t_end:
+                pass
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g.replay()
+        torch.cuda.synchronize()
+        res.setdefault(mode, []).append((time.perf_counter() - t0) * 1e6 / K)
     print("plain sorted:", " ".join(f"{x:.1f}" for x in sorted(res["plain"])))
+    for mode in ("bench", "bench+spin"):
+        print(mode, " ".join(f"{x:.1f}" for x in res.pop(mode)))
     for k, v in res.items():
         print(f"{k:9s} host us/step median {statistics.median(v):7.2f}  min {min(v):7.2f}"
               + (f"  | device us/step median {statistics.median(dev[k]):7.2f}" if k in dev else ""))
