@@ -1004,6 +1004,14 @@ def run_steps(args, ep, pool, use_graph, world, device):
         run_k()
         ran += args.steps
     torch.cuda.synchronize()
+    # one more untimed replay, waited for at once: the host's last wait before
+    # the timed region is then one replay long, not the ~10 ms of the warm
+    # replays — after a long blocking wait the timed replay's launches reach
+    # the GPU late (kernel trace: 28-31.5 us kernels starting 34-38 us apart).
+    # Same box, 4 interleaved pairs at K = 20: 33.0-33.6 vs 33.5-34.3 us per
+    # step (profiles/r05/driver_ab.txt)
+    run_k()
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
