@@ -84,10 +84,12 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         g.replay()
+        t_sub = time.perf_counter()
         torch.cuda.synchronize()
         res.setdefault(mode, []).append((time.perf_counter() - t0) * 1e6 / K)
+        res.setdefault(mode + " submit", []).append((t_sub - t0) * 1e6 / K)
     print("plain sorted:", " ".join(f"{x:.1f}" for x in sorted(res["plain"])))
-    for mode in ("bench", "bench+spin"):
+    for mode in ("bench", "bench+spin", "bench submit", "bench+spin submit"):
         print(mode, " ".join(f"{x:.1f}" for x in res.pop(mode)))
     for k, v in res.items():
         print(f"{k:9s} host us/step median {statistics.median(v):7.2f}  min {min(v):7.2f}"
