@@ -102,6 +102,10 @@ def parse():
                          "fixed graph-launch + sync cost (~0.2 ms) is amortised; 50 for F/G)")
     ap.add_argument("--warmup", type=int, default=None,
                     help="untimed steps first (default 20; 1 scenario run for workload A)")
+    ap.add_argument("--ramp-seconds", type=float, default=0.4,
+                    help="untimed replays of the K steps before the timed region run for at "
+                         "least this long (and >= 300 steps): HBM-bound steps speed up over "
+                         "the first ~0.1-0.3 s of sustained work (profiles/r05/clock_replay.txt)")
     ap.add_argument("--workload", default="C", choices=sorted(WORKLOADS))
     ap.add_argument("--integrator", default=None,
                     choices=["rect+cum", "rect+rot", "rect", "qk21+rot", "qk21"],
@@ -999,11 +1003,26 @@ def run_steps(args, ep, pool, use_graph, world, device):
                 step(i)
             flush()
 
-    ran = 0
-    while ran < 300:                         # untimed: the clock ramp
-        run_k()
-        ran += args.steps
-    torch.cuda.synchronize()
+    # untimed: the clock ramp. At least 300 steps and ramp_seconds of wall
+    # time; the host waits every ~2 ms of queued work so that it never runs
+    # far ahead of the GPU. Repeated K=20 replays, each after a sync, take
+    # 33-34 us per step for the first ~0.1-0.3 s of a process's work and
+    # 28.5-29 after it (profiles/r05/clock_replay.txt).
+    # Every rank runs the same number of replays (the exchange steps are
+    # collective): the ranks agree on going on (MAX of their flags).
+    ran, t_ramp = 0, time.perf_counter()
+    while True:
+        for _ in range(max(1, 64 // args.steps)):
+            run_k()
+            ran += args.steps
+        torch.cuda.synchronize()
+        more = ran < 300 or time.perf_counter() - t_ramp < getattr(args, "ramp_seconds", 0.0)
+        if world > 1:
+            f = torch.tensor([1.0 if more else 0.0], dtype=torch.float64, device=device)
+            dist.all_reduce(f, op=dist.ReduceOp.MAX)
+            more = float(f.item()) > 0
+        if not more:
+            break
     # one more untimed replay, waited for at once: the host's last wait before
     # the timed region is then one replay long, not the ~10 ms of the warm
     # replays — after a long blocking wait the timed replay's launches reach
