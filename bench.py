@@ -6,8 +6,11 @@
 
 Workloads:
   C (default)  N=10 horizon, 1e6 candidates per GPU, moving-target episode
-               (reference operator schedule), grid regenerated per step and
-               sampled on device; weak scaling: 1e6 x G candidates over G GPUs
+               (reference operator schedule); by default each step's candidate
+               batch is already resident in HBM (--inputs resident; the grid
+               regenerated per step around the chosen control and sampled on
+               device is --inputs sampled / generated, both also reported in
+               the line); weak scaling: 1e6 x G candidates over G GPUs
   B            N=3, 1e5 candidates per GPU, same episode machinery
   D            N=12, 1.25e6 candidates per GPU (1e7 over 8), one exchange/step
   E            1024 robots x 1e4 candidates, N=8, batched per-robot arg-min,
@@ -55,6 +58,7 @@ sys.path.insert(0, REPO)
 
 METRIC = "candidate N-step rollouts/sec + MPC-step p50 latency, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+D_TOTAL = 10_000_000    # config D's candidate total (BASELINE.json configs[3])
 
 WORKLOADS = {
     "A": dict(n_steps=3, per_gpu=None,
@@ -130,13 +134,15 @@ def parse():
                          "MPC_LAYOUT_TILED (each 512-candidate tile's horizon contiguous in HBM, "
                          "include/mpc_rollout.h), soa = the step-major SoA every entry accepts")
     ap.add_argument("--no-config-d", action="store_true",
-                    help="workload C: skip the config-D sub-result (N=12, 1.25e6 candidates "
-                         "per GPU, the BASELINE multi-GPU config) measured in the same run")
-    ap.add_argument("--parity-steps", type=int, default=8,
-                    help="chained episode workloads: after the timed regions, log this many "
-                         "steps of a fresh episode and re-scan each on the host with the CPU "
-                         "oracle in the reference's arithmetic (qk21): the line's `parity` "
-                         "(0 = skip)")
+                    help="workload C: skip the config-D sub-results measured in the same run "
+                         "(N=12; config_d: 1.25e6 candidates per GPU, weak; config_d_total: "
+                         "1e7 in total over the N GPUs, strong — BASELINE's multi-GPU config)")
+    ap.add_argument("--parity-steps", type=int, default=116,
+                    help="chained episode workloads: after the timed regions, the checker "
+                         "legs of parity_pass (oracle/parity.py) against the CPU oracle in "
+                         "the reference's arithmetic (qk21): the line's `parity`.  One GPU: "
+                         "this many steps of the episode leg (default 116: the reference's "
+                         "events at p = 60 / 90 / 110 and a restart); 0 = skip every leg")
     ap.add_argument("--fused", action="store_true",
                     help="one launch per step: the rollout's last block runs the selection "
                          "(mpc_episode_rollout) instead of a separate selection launch")
@@ -502,9 +508,39 @@ def main():
             "workload", "n_steps", "candidates_per_gpu", "candidates_total", "launch",
             "parallelism")}
         assert getattr(ep, "p2p", False) == ep_form or world == 1, "config D changed form"
+        # BASELINE config D as written: 1e7 candidates IN TOTAL over the N
+        # ranks (strong scaling: 1e7 on one GPU at N = 1, 1.25e6 per GPU at 8)
+        del pool
+        finish_episode(ep)
+        del ep
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        t_args = argparse.Namespace(**vars(args))
+        t_args.candidates_per_gpu = -(-D_TOTAL // world)
+        t_out, ep, pool = bench_episode(t_args, WORKLOADS["D"], eng, rank, world, device, None,
+                                        sub=True)
+        out["config_d_total"] = {k: t_out[k] for k in (
+            "value", "unit", "ms_per_step", "p50_ms", "p90_ms", "chain_error", "exchange",
+            "kernel_ms", "roofline", "roofline_valu", "ramp")}
+        out["config_d_total"]["scaling"] = "strong"
+        out["config_d_total"]["config"] = {k: t_out["config"][k] for k in (
+            "workload", "n_steps", "candidates_per_gpu", "candidates_total", "launch",
+            "parallelism")}
+        out["config_d_total"]["config"]["workload"] = (
+            "config D as BASELINE.json states it: N=12, 1e7 candidates in total sharded over "
+            "the N GPUs (contiguous index ranges; one exchange per step at N > 1)")
+        out["config_d"]["scaling"] = "weak"
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out, default=_plain), flush=True)
     finish(ep, world > 1 or args.exchange)
+
+
+def _plain(o):
+    """json default: numpy scalars (the checker's comparisons) as Python ones."""
+    import numpy as np
+    if isinstance(o, np.generic):
+        return o.item()
+    raise TypeError(f"not JSON serializable: {type(o).__name__}")
 
 
 def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
@@ -646,6 +682,11 @@ def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
     out = {
         "metric": METRIC, "value": value, "unit": "rollouts/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
+        "ramp": {"steps": main_run["ramp_steps"], "seconds": main_run["ramp_s"],
+                 "note": "untimed replays of the K steps after the W warmup steps and before "
+                         "the timed region (>= 300 steps and >= --ramp-seconds): the GPU's "
+                         "clocks ramp over the first ~0.1-0.3 s of sustained work "
+                         "(profiles/r05/clock_replay.txt); the timed region is sustained state"},
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": wl["desc"], "n_steps": n_steps,
@@ -723,81 +764,185 @@ def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
 
 
 def parity_pass(args, eng, ep, pool, rank, world, device):
-    """CHECKER, run after every timed region and never timed: the identity of
-    the bench's chosen controls with the reference's arithmetic at full size
-    (SURVEY §7 hard part 2).  A fresh episode of the bench's own form (same
-    shard, step form and exchange) logs --parity-steps chained steps over the
-    first resident batches; every step's problem is rebuilt on the host from
-    the log (episode.logged_step_problems) and each rank re-scans its shard
-    with the CPU oracle in qk21 mode (scipy quad's 21-point Kronrod sums, glibc
-    trig, the reference's operation order: oracle/mpc_oracle.c, pinned bitwise
-    to the reference's own outputs); the ranks' lexicographic (cost, index)
-    minima give the oracle's global winner.  identity_rate: the share of
-    steps whose logged winner is the oracle's; for mismatches the oracle's own
-    relative cost gap between the two (max_rel_dcost_mismatch); and the
-    largest relative difference between the logged cost and the oracle's cost
-    of the same candidate (the two arithmetics' noise)."""
+    """CHECKER, run after every timed region and never timed: the hot path's
+    forms of this run against the CPU oracle in the reference's arithmetic
+    (qk21: scipy quad's 21-point Kronrod sums, glibc trig, the reference's
+    operation order — oracle/mpc_oracle.c, pinned bitwise to the reference's
+    own outputs).  Legs (oracle/parity.py):
+      episode      a fresh device episode of the bench's own step form (same
+                   shard, chained launch, layout and exchange) over the first
+                   resident batches, through the operator events and a
+                   restart (one GPU: the reference schedule p = 60 / 90 / 110
+                   with a step limit of 112, 116 steps; N > 1: p = 6 / 12 / 16,
+                   limit 20, 24 steps), against an INDEPENDENT oracle episode
+                   that scans each batch itself from ITS OWN previous winner:
+                   index, (v, beta), returned pose, status bits per step
+                   (math_model_tree.py:351-359,392-414,542-569);
+      sampler      the first resident batch (tiled sampler) and 3 steps of a
+                   sampled-mode episode (the device sampler on the grid around
+                   the chosen control), bitwise against the oracle sampler,
+                   and those steps' winners (:239-256,312-316);
+      fulltree     one S1 = 451 full-tree step (run_math_model.py:156-197),
+                   device qk21 and rect+rot vs the oracle's scan;
+      ft_episodes  8 of run_math_model.py's episodes (:231-280), device
+                   resident (mpc_fulltree_episodes_run) vs the oracle;
+      tree_episodes the named entry over the tree expansion (mpc_episodes_run)
+                   vs the oracle.
+    Every rank checks its own shard; the ranks' lexicographic (cost, index)
+    minima give the oracle's global winner."""
+    import math as _m
     import numpy as np
     import torch
     import torch.distributed as dist
-    from concurrent.futures import ThreadPoolExecutor
-    from oracle import oracle as O
-    from diplomjourney_amd.episode import DeviceEpisode, logged_step_problems
-    K = min(args.parity_steps, len(pool))
+    from oracle import parity as P
+    from diplomjourney_amd import math_model_tree as mmt
+    from diplomjourney_amd.episode import DeviceEpisode
     t_start = time.perf_counter()
-    fresh = DeviceEpisode(eng, ep.n_total, ep.n_steps, rank=rank, world=world,
-                          integrator=ep.integrator, group=ep.group, log_capacity=max(64, K),
-                          exchange=ep.exchange, chain=True, p2p=getattr(ep, "p2p", False))
-    for i in range(K):
-        fresh.step(controls=pool[i])
-    fresh.flush()
-    log = fresh.read_log()
-    probs = logged_step_problems(log, fresh.cfg)
     try:
         threads = max(1, min(16, len(os.sched_getaffinity(0)) // max(1, world)))
     except AttributeError:
         threads = 4
-    rows = np.full((K, 4), np.nan)     # best cost, best global index, cost at the logged index
-    with ThreadPoolExecutor(max_workers=threads) as ex:
-        futs = []
-        for i in range(K):
-            vh, bh = (a.cpu().numpy() for a in soa_pool(fresh, pool[i:i + 1])[0])
-            futs.append(ex.submit(O.rollout_argmin, probs[i][0], vh, bh, index_base=fresh.lo,
-                                  incumbent=probs[i][1], integ="qk21", want_costs=True))
-        for i, f in enumerate(futs):
-            ref, costs, _ = f.result()
-            rows[i, 0], rows[i, 1] = ref.cost, ref.index
-            j = log[i].index - fresh.lo
-            if 0 <= j < fresh.n_local:
-                rows[i, 2] = costs[j]
-            rows[i, 3] = float(ref.found)
-    finish_episode(fresh)
-    if world > 1:
-        on_dev = dist.get_backend() == "nccl"
-        t = torch.from_numpy(rows).to(device if on_dev else "cpu")
-        allr = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(allr, t)
-        per = np.stack([a.cpu().numpy() for a in allr])          # [world, K, 4]
+    on_dev = dist.is_initialized() and dist.get_backend() == "nccl"
+
+    def allgather(a):
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        if world == 1:
+            return a[None]
+        t = torch.from_numpy(a).to(device if on_dev else "cpu")
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+        return np.stack([o.cpu().numpy() for o in outs])
+
+    # -- episode: the bench's own chained form through events and a restart --
+    if world == 1:
+        sched = dict(p_turn_right=60, p_turn_left=90, p_new_target=110, max_steps=112)
+        K = args.parity_steps if args.parity_steps > 0 else 116
     else:
-        per = rows[None]
-    same, gaps, noise = 0, [], 0.0
+        sched = dict(p_turn_right=6, p_turn_left=12, p_new_target=16, max_steps=20)
+        K = 24
+    nb = min(8, len(pool))
+    fresh = DeviceEpisode(eng, ep.n_total, ep.n_steps, rank=rank, world=world,
+                          integrator=ep.integrator, group=ep.group, log_capacity=max(64, K),
+                          exchange=ep.exchange, chain=True, p2p=getattr(ep, "p2p", False),
+                          max_steps=sched["max_steps"])
+    for k, v in sched.items():
+        setattr(fresh.cfg, k, v)
+    fresh.reset()                        # the state takes the schedule
     for i in range(K):
-        best = min(range(world), key=lambda r: (per[r, i, 0], per[r, i, 1]))
-        c_best, i_best = per[best, i, 0], int(per[best, i, 1])
-        c_logged = np.nanmin(per[:, i, 2])       # the one rank holding the logged index
-        if log[i].index == i_best:
-            same += 1
-            noise = max(noise, abs(log[i].cost - c_best) / abs(c_best))
-        else:
-            gaps.append(float(abs(c_logged - c_best) / abs(c_best)))
-    return {"steps": K, "identity_rate": same / K, "mismatches": len(gaps),
-            "max_rel_dcost_mismatch": max(gaps) if gaps else 0.0,
-            "max_rel_cost_diff_identical": noise,
-            "oracle": "qk21 (the reference's scipy quad arithmetic), oracle/mpc_oracle.c",
-            "threads_per_rank": threads, "check_s": time.perf_counter() - t_start,
-            "note": "checker after the timed regions: a fresh episode of the bench's step "
-                    "form over the first resident batches, each step re-scanned in full on "
-                    "the host; not part of any timed value"}
+        fresh.step(controls=pool[i % nb])
+    fresh.flush()
+    log = fresh.read_log()
+    cfg = fresh.cfg
+    finish_episode(fresh)
+    del fresh
+    host = [(v.cpu().numpy(), b.cpu().numpy()) for v, b in soa_pool(ep, pool, nb)]
+    scanners = [P.ShardScanner(v, b, ep.lo, threads) for v, b in host]
+    out = {"episode": P.episode_leg((cfg, log), None, scanners, allgather, threads)}
+    out["episode"]["schedule"] = sched
+    del scanners
+
+    # -- sampler: the resident batch, then sampled-mode steps -----------------
+    V0 = mmt.vector_of_velocities(0.5)
+    B0 = mmt.vector_of_beta_angles(0.0)
+    ov, ob = O_sample(V0, B0, ep.n_local, ep.n_steps, 0x5EED0000, ep.lo)
+    pool_bitwise = bool(np.array_equal(ov, host[0][0]) and np.array_equal(ob, host[0][1]))
+    del host, ov, ob
+    samp = DeviceEpisode(eng, ep.n_total, ep.n_steps, rank=rank, world=world,
+                         integrator=ep.integrator, group=ep.group, log_capacity=64,
+                         exchange=ep.exchange, chain=False)
+    drawn = []
+    for _ in range(3):
+        samp.step()
+        drawn.append((samp.v_sc.cpu().numpy(), samp.b_sc.cpu().numpy()))
+    slog = samp.read_log()
+    s = P.sampled_leg(samp.cfg, drawn, slog, ep.n_local, ep.n_steps, ep.lo, allgather, threads)
+    finish_episode(samp)
+    del samp, drawn
+    s["resident_batch_bitwise"] = bool(np.all(allgather(np.array([float(pool_bitwise)])) == 1.0))
+    out["sampler"] = s
+
+    # -- full tree: one S1 = 451 step (workload F's grid and first call) ------
+    from diplomjourney_amd import run_math_model as rmm
+    from diplomjourney_amd.abi import MpcFulltreeProblem
+    from diplomjourney_amd.expansion import fulltree_argmin, fulltree_result
+    rmm.configure(0.1, _m.radians(3))
+    try:
+        Vf, Bf = np.asarray(rmm.vector_v, dtype=np.float64), np.asarray(rmm.vector_beta,
+                                                                        dtype=np.float64)
+        st, tg = (-3.0, -2.0, 0.3), (4.0, 5.0)
+        atan_t = float(np.arctan(tg[0] / tg[1]))
+        inc = P._ft_criterion0(*st, *tg)
+        vg = torch.tensor(Vf, device=eng.device)
+        bg = torch.tensor(Bf, device=eng.device)
+        fp = MpcFulltreeProblem(*st, *tg, st[0], st[1], atan_t, float(rmm.L), 0.05, 0.1)
+        dev = {}
+        for integ in ("qk21", "rect+rot"):
+            r = fulltree_result(fulltree_argmin(eng, fp, vg, bg, inc, integ))
+            dev[integ] = (r.leaf, r.cost, r.found, r.trajectory())
+        out["fulltree"] = P.fulltree_leg(dev, Vf, Bf, (st, tg, st[:2], atan_t, float(rmm.L),
+                                                       0.05, 0.1), inc, rank, world, allgather,
+                                         threads)
+        # -- the script's episodes, device resident (workload G's grid) -------
+        rmm.configure(0.25, _m.radians(10))
+        starts = rmm.draw_starts(8, seed=20261015)
+        t0 = time.perf_counter()
+        ref = P.ft_episodes_oracle(starts, np.asarray(rmm.vector_v, dtype=np.float64),
+                                   np.asarray(rmm.vector_beta, dtype=np.float64), float(rmm.L),
+                                   float(rmm.delta_t), float(rmm.eps), 4, threads)
+        fe = {}
+        for integ in ("qk21", "rect+rot"):
+            d = rmm.run_batched(starts, max_calls=4, integrator=integ)
+            fe[integ] = P.compare_episodes(
+                [([r["ret"] + [r["optimal_criterion"]] for r in recs], stop) for recs, stop in d],
+                ref)
+        fe["s1"] = int(rmm.size_max_1)
+        fe["check_s"] = time.perf_counter() - t0
+        out["ft_episodes"] = fe
+    finally:
+        rmm.configure()
+    # -- the named entry over the tree expansion (workload R's engine) -------
+    starts = rmm.draw_starts(8, seed=20261016)
+    t0 = time.perf_counter()
+    d = rmm.run_tree_batched(starts, max_calls=12, integrator="qk21", engine=eng)
+    te = P.compare_episodes(d, P.tree_episodes_oracle(starts, 12, threads))
+    te["check_s"] = time.perf_counter() - t0
+    out["tree_episodes"] = te
+
+    e, sm, ft = out["episode"], out["sampler"], out["fulltree"]
+    fq = out["ft_episodes"]["qk21"]
+    checks = {
+        "episode_identity": e["identity_rate"] == 1.0,
+        "episode_v_beta": e["v_beta_identical_rate"] == 1.0,
+        "episode_pose_le_1e-6": e["max_abs_pose_diff"] <= 1e-6,
+        "episode_status": e["status_identical_rate"] == 1.0 and e["p_episode_identical_rate"] == 1.0,
+        "episode_events_and_restart": e["event_steps"] >= 1 and e["restarts"] >= 1,
+        "sampler_bitwise": sm["batches_bitwise"] and sm["resident_batch_bitwise"],
+        "sampled_identity": sm["identity_rate"] == 1.0 and sm["max_abs_pose_diff"] <= 1e-6,
+        "fulltree_qk21": ft["qk21"]["leaf_identical"] and ft["qk21"]["max_abs_state_diff"] <= 1e-9,
+        "ft_episodes_qk21": (fq["stops_identical"] and fq["calls_identical"]
+                             and fq["v_beta_identical_rate"] == 1.0
+                             and fq["max_abs_pose_diff"] <= 1e-9),
+        "tree_episodes_qk21": (te["stops_identical"] and te["calls_identical"]
+                               and te["v_beta_identical_rate"] == 1.0
+                               and te["max_abs_pose_diff"] <= 1e-9),
+    }
+    out.update({
+        "steps": e["steps"], "identity_rate": e["identity_rate"],
+        "max_abs_pose_diff": e["max_abs_pose_diff"], "checks": checks,
+        "pass": all(checks.values()),
+        "oracle": "qk21 (the reference's scipy quad arithmetic), oracle/mpc_oracle.c; episode "
+                  "bookkeeping restated in oracle/parity.py",
+        "threads_per_rank": threads, "check_s": time.perf_counter() - t_start,
+        "note": "checker after the timed regions, not part of any timed value; rect+rot rows "
+                "are the kernels' other arithmetic against the same qk21 oracle (reported, "
+                "not gated)"})
+    return out
+
+
+def O_sample(V, B, n, n_steps, seed, lo):
+    """The oracle sampler (checker only)."""
+    from oracle import oracle as O
+    return O.sample_controls(V, B, n, n_steps, seed, index_base=lo)
 
 
 def finish_episode(ep):
@@ -1030,7 +1175,9 @@ def run_steps(args, ep, pool, use_graph, world, device):
     # Same box, 4 interleaved pairs at K = 20: 33.0-33.6 vs 33.5-34.3 us per
     # step (profiles/r05/driver_ab.txt)
     run_k()
+    ran += args.steps
     torch.cuda.synchronize()
+    ramp_s = time.perf_counter() - t_ramp
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -1073,7 +1220,8 @@ def run_steps(args, ep, pool, use_graph, world, device):
         fl[i][1].record()
     torch.cuda.synchronize()
     flush_ms = (sum(a.elapsed_time(b) for a, b in fl) / n_kern) if has_flush else 0.0
-    return {"elapsed": elapsed, "graph": graph is not None,
+    return {"elapsed": elapsed, "graph": graph is not None, "ramp_steps": ran,
+            "ramp_s": ramp_s,
             "kernel_timed_ms": max(timed_ms - flush_ms, 0.0) / args.steps,
             "flush_ms": flush_ms,
             "p50_ms": percentile(step_gpu_ms, 50),

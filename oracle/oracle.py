@@ -51,6 +51,10 @@ def lib():
         L.mpc_oracle_fulltree_argmin.argtypes = (
             [_P, ctypes.c_int32, _P, ctypes.c_int32] + [_D] * 12 + [ctypes.c_int32]
             + [ctypes.POINTER(_D), ctypes.POINTER(ctypes.c_int32), _P, _P, _P, _P, _P])
+        L.mpc_oracle_fulltree_argmin_range.restype = ctypes.c_int64
+        L.mpc_oracle_fulltree_argmin_range.argtypes = (
+            [_P, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64] + [_D] * 11
+            + [ctypes.c_int32, ctypes.POINTER(_D), _P])
         L.mpc_oracle_sample_controls.restype = None
         L.mpc_oracle_sample_controls.argtypes = [
             _P, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
@@ -156,3 +160,19 @@ def fulltree_argmin(V, B, state, target, origin, atan_target, L, t_a, t_b, incum
     if detail:
         out.update(costs=arrs[0], leaf_states=arrs[1], layer0=arrs[2], layer1=arrs[3])
     return out
+
+
+def fulltree_argmin_range(V, B, k0_lo, k0_hi, state, target, origin, atan_target, L, t_a, t_b,
+                          integ=MPC_INTEG_QK21):
+    """The slice k0 in [k0_lo, k0_hi) of fulltree_argmin's scan (global leaf
+    indices; the slices' lexicographic (cost, leaf) minimum is the whole
+    scan's first minimum).  Returns (leaf or -1, cost, traj[3][3])."""
+    V = np.ascontiguousarray(V, dtype=np.float64)
+    B = np.ascontiguousarray(B, dtype=np.float64)
+    res = np.zeros(9)
+    best = _D()
+    leaf = lib().mpc_oracle_fulltree_argmin_range(
+        _ptr(V), len(V), _ptr(B), len(B), int(k0_lo), int(k0_hi), state[0], state[1], state[2],
+        target[0], target[1], origin[0], origin[1], atan_target, L, t_a, t_b, _integ(integ),
+        ctypes.byref(best), _ptr(res))
+    return int(leaf), best.value, res.reshape(3, 3).tolist()
