@@ -1187,8 +1187,9 @@ __device__ void p2p_complete(const mpc_episode_config_t& c, EpisodeState* S, voi
   __shared__ uint32_t s_err, s_seq;
   const uint64_t my_peer = static_cast<int>(threadIdx.x) < world ? hdr->peers[threadIdx.x] : 0;
   const int my_rank = threadIdx.x == 0 ? hdr->rank : 0;
-  // an earlier step of this episode already timed out (a peer gone): fail
-  // fast instead of waiting the full budget again on every later step
+  // an earlier step of this episode already timed out waiting for its peers
+  // (error 5: a peer gone): fail fast instead of waiting the full budget
+  // again on every later step.  Other errors say nothing about the peers.
   const uint32_t prior_err = threadIdx.x == 0 ? S->chain_error : 0u;
   const uint32_t seq = threadIdx.x == 0 ? S->p2p_seq : 0u;
   mpc_candidate_t* lc = cand_lds();
@@ -1204,7 +1205,7 @@ __device__ void p2p_complete(const mpc_episode_config_t& c, EpisodeState* S, voi
   const uint32_t slot = s_seq & 1u;
   post_candidate(s_peers, s_rank, world, prev, slot, n_steps, lc);
   const mpc_candidate_t* g =
-      wait_mailbox(S, mb, prev, slot, world, n_steps, s_err ? 0ull : kPeerWaitTicks);
+      wait_mailbox(S, mb, prev, slot, world, n_steps, s_err == 5u ? 0ull : kPeerWaitTicks);
   if (threadIdx.x == 0) S->p2p_seq = s_seq + 1u;   // read by the next launch
   if (g) {
     advance_from_candidates<INTEG, ROT>(c, S, g, world, out_prev, log, cap, publish_epoch,

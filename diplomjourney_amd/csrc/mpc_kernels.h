@@ -1538,9 +1538,10 @@ __device__ void sample_items(const double2* s_grid, uint32_t n_grid, int64_t n_c
         const int64_t o = tiled ? ctl_off<true>(st, c, ld) : ctl_off<false>(st, c, ld);
         *reinterpret_cast<double2*>(v + o) = make_double2(e0.x, e1.x);
         *reinterpret_cast<double2*>(b + o) = make_double2(e0.y, e1.y);
-      } else {
-        v[st * ld + c] = e0.x;
-        b[st * ld + c] = e0.y;
+      } else {   // one candidate per item: the same layout choice as the pairs
+        const int64_t o = tiled ? ctl_off<true>(st, c, ld) : ctl_off<false>(st, c, ld);
+        v[o] = e0.x;
+        b[o] = e0.y;
       }
     }
   }

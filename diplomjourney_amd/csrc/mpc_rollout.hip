@@ -120,6 +120,24 @@ bool chain_ctl_ok(const double* v, const double* b, int64_t n_cand, int32_t inte
   return is_tiled(integrator) ? tiled_ok(v, b, n_cand) : wide_ok(v, b, n_cand);
 }
 
+// The bounded device waits count wall_clock64 ticks at kWallHz
+// (mpc_episode.h).  A device whose constant-rate clock runs at another rate
+// would scale every budget silently: the entries with such waits refuse it.
+// Unknown (no device / the query fails): not refused here (the launch reports).
+bool wall_clock_ok() {
+  static int cache[16] = {0};   // 0 unknown, 1 kWallHz, -1 another rate
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return true;
+  if (cache[dev] == 0) {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+        khz <= 0)
+      return true;
+    cache[dev] = static_cast<uint64_t>(khz) * 1000ull == kWallHz ? 1 : -1;
+  }
+  return cache[dev] == 1;
+}
+
 template <class F>
 void dispatch_mode(int32_t integrator, F&& f) {
   const bool rot = (integrator & MPC_HEADING_ROTATE) != 0;
@@ -633,6 +651,7 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
       return MPC_ERR_ARG;
     has_prev = 1;
   }
+  if (!wall_clock_ok()) return MPC_ERR_UNSUPPORTED;
   EpisodeState* S = static_cast<EpisodeState*>(state);
   int e;
   const int pl2 = frexp(cfg->L, &e) == 0.5 ? 1 : 0;   // as consts_from_problem decides
@@ -688,6 +707,7 @@ int mpc_episode_exchange_step2(const mpc_episode_config_t* cfg, void* state, uin
   if (mode_ok(integrator) != MPC_OK || !is_cum(integrator) || !wide_ok(v_sc, beta_sc, n_cand))
     return MPC_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
+  if (!wall_clock_ok()) return MPC_ERR_UNSUPPORTED;
   EpisodeState* S = static_cast<EpisodeState*>(state);
   int e;
   const int pl2 = frexp(cfg->L, &e) == 0.5 ? 1 : 0;
@@ -863,8 +883,18 @@ int mpc_mailbox_set_peers(void* mailbox, int32_t rank, int32_t world, const void
 
 int mpc_mailbox_ping(void* mailbox, uint32_t tag, int32_t* ok, mpc_stream_t stream) {
   if (!mailbox || !ok || tag == 0) return MPC_ERR_ARG;
+  if (!wall_clock_ok()) return MPC_ERR_UNSUPPORTED;
   k_mailbox_ping<<<1, 64, 0, reinterpret_cast<hipStream_t>(stream)>>>(mailbox, tag, ok);
   return last_hip_status();
+}
+
+int mpc_mailbox_clear(void* mailbox, int32_t world, mpc_stream_t stream) {
+  if (!mailbox || world < 1 || world > kMailMaxRanks) return MPC_ERR_ARG;
+  return hipMemsetAsync(static_cast<char*>(mailbox) + kMailHdrBytes, 0,
+                        mailbox_bytes(world) - kMailHdrBytes,
+                        reinterpret_cast<hipStream_t>(stream)) == hipSuccess
+             ? MPC_OK
+             : MPC_ERR_HIP;
 }
 
 int mpc_episode_p2p_step(const mpc_episode_config_t* cfg, void* state, uint32_t epoch,
@@ -888,6 +918,7 @@ int mpc_episode_p2p_step(const mpc_episode_config_t* cfg, void* state, uint32_t 
       (prev_epoch && !chain_ctl_ok(v_prev, beta_prev, n_cand, integrator)))
     return MPC_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
+  if (!wall_clock_ok()) return MPC_ERR_UNSUPPORTED;
   EpisodeState* S = static_cast<EpisodeState*>(state);
   int e;
   const int pl2 = frexp(cfg->L, &e) == 0.5 ? 1 : 0;
@@ -929,6 +960,7 @@ int mpc_episode_p2p_flush(const mpc_episode_config_t* cfg, void* state, uint32_t
       !chain_ctl_ok(v_last, beta_last, n_cand, integrator))
     return MPC_ERR_UNSUPPORTED;
   if (ws_bytes < mpc_workspace_bytes(n_cand, n_steps)) return MPC_ERR_WORKSPACE;
+  if (!wall_clock_ok()) return MPC_ERR_UNSUPPORTED;
   auto launch = [&](auto tiled_tag) {
     constexpr bool T = decltype(tiled_tag)::value;
     k_episode_p2p_flush<MPC_INTEG_RECT, kRotCum, T>

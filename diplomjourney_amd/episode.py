@@ -21,6 +21,7 @@ import ctypes
 import math
 import sys
 import time
+import weakref
 
 import torch
 
@@ -383,7 +384,7 @@ class DeviceEpisode:
         self._epoch = 0
         self._checked = {}
         self.steps_enqueued = 0
-        self.reset()
+        self.reset(_fresh_mailbox=True)
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -485,11 +486,24 @@ class DeviceEpisode:
             L.mpc_mailbox_free(ctypes.c_void_p(self._mailbox))
             self._mailbox = None
 
-    def reset(self):
+    def reset(self, _fresh_mailbox=False):
+        """Restart the episode from cfg.  P2P form: also zeroes this rank's
+        mailbox slots (mpc_mailbox_clear), so that no step replayed with an
+        epoch of the previous run (a graph captured before the reset) reads a
+        stale candidate as fresh; with world > 1 that makes reset() a
+        collective — every rank calls it, and none posts into a peer's
+        mailbox before every rank has cleared its own.  (A new mailbox is
+        zeroed by mpc_mailbox_alloc.)"""
         native.check(self.lib.mpc_episode_reset(ctypes.byref(self.cfg), self.state.data_ptr(),
                                                 self._stream()), "mpc_episode_reset")
         self.steps_enqueued = 0
         self._pending = None
+        if self.p2p and self._mailbox and not _fresh_mailbox:
+            native.check(self.lib.mpc_mailbox_clear(ctypes.c_void_p(self._mailbox), self.world,
+                                                    self._stream()), "mpc_mailbox_clear")
+            if self.world > 1:
+                torch.cuda.current_stream().synchronize()
+                self._all_ok(1, self.state.device)      # every rank cleared
 
     @staticmethod
     def _is_tiled(controls):
@@ -505,12 +519,28 @@ class DeviceEpisode:
         v, b = controls
         return v.data_ptr(), b.data_ptr(), self._integ
 
+    def _seen(self, key, *tensors):
+        """Was this very batch (same tensor objects) checked before?  The cache
+        holds weak references only: a caller's per-step batches are not kept
+        alive by it (and a new tensor reusing a freed one's id and memory is
+        not mistaken for it)."""
+        refs = self._checked.get(key)
+        return refs is not None and all(r() is t for r, t in zip(refs, tensors))
+
+    def _remember(self, key, *tensors):
+        if len(self._checked) >= 4096:
+            self._checked = {k: r for k, r in self._checked.items()
+                             if all(x() is not None for x in r)}
+            if len(self._checked) >= 4096:
+                self._checked.clear()
+        self._checked[key] = tuple(weakref.ref(t) for t in tensors)
+
     def _check_controls(self, controls):
         if self._is_tiled(controls):
             return self._check_tiled(controls)
         v, b = controls
         key = (id(v), id(b), v.data_ptr(), b.data_ptr())
-        if key in self._checked:         # a resident batch seen before: checked once
+        if self._seen(key, v, b):        # a resident batch seen before: checked once
             return v, b
         if (tuple(v.shape) != (self.n_steps, self.n_local) or v.shape != b.shape
                 or v.dtype != torch.float64 or b.dtype != torch.float64
@@ -518,14 +548,13 @@ class DeviceEpisode:
                 or v.device != self.v_sc.device or b.device != self.v_sc.device):
             raise ValueError("controls must be contiguous float64 [n_steps, n_local] "
                              "tensors on the episode's device")
-        if len(self._checked) < 4096:
-            self._checked[key] = (v, b)   # holds the tensors: ids stay unique
+        self._remember(key, v, b)
         return v, b
 
     def _check_tiled(self, t):
         from .abi import MPC_TILE
         key = (id(t), t.data_ptr())
-        if key in self._checked:
+        if self._seen(key, t):
             return t
         if (tuple(t.shape) != (-(-self.n_local // MPC_TILE), self.n_steps, 2, MPC_TILE)
                 or t.dtype != torch.float64 or not t.is_contiguous()
@@ -533,8 +562,7 @@ class DeviceEpisode:
             raise ValueError("tiled controls must be a contiguous 16-B aligned float64 "
                              "[ceil(n_local / 512), n_steps, 2, 512] tensor on the episode's "
                              "device (Expansion.sample_controls_tiled)")
-        if len(self._checked) < 4096:
-            self._checked[key] = t
+        self._remember(key, t)
         return t
 
     def _chain_step(self, controls, events=None):
@@ -919,13 +947,26 @@ class DeviceFtEpisodes:
                      "mpc_fulltree_episodes_reset")
         self.progress.zero_()
 
+    # leaves one block may score in one launch (a robot's calls x S1^3): ~1 s
+    # of qk21 arithmetic per block, far below the driver's compute-lockup
+    # timeout whatever S1 and max_calls the caller asks for
+    LEAF_BUDGET = 1 << 30
+
     def run(self, max_calls):
-        """Enqueue up to max_calls MPC calls of every still-running robot."""
-        native.check(self.lib.mpc_fulltree_episodes_run(
-            self.state.data_ptr(), self.R, self.vg.data_ptr(), self.vg.numel(),
-            self.bg.data_ptr(), self.bg.numel(), self.L, self.delta_t, self.eps, self._integ,
-            int(max_calls), self.log.data_ptr(), self.log_capacity, self.progress.data_ptr(),
-            _stream()), "mpc_fulltree_episodes_run")
+        """Enqueue up to max_calls MPC calls of every still-running robot: as
+        few launches as LEAF_BUDGET allows (chunked launches continue the
+        episodes exactly as one launch would)."""
+        s1 = self.vg.numel() * self.bg.numel()
+        per = max(1, min(int(max_calls), self.LEAF_BUDGET // max(1, s1 ** 3)))
+        left = int(max_calls)
+        while left > 0:
+            n = min(per, left)
+            native.check(self.lib.mpc_fulltree_episodes_run(
+                self.state.data_ptr(), self.R, self.vg.data_ptr(), self.vg.numel(),
+                self.bg.data_ptr(), self.bg.numel(), self.L, self.delta_t, self.eps,
+                self._integ, n, self.log.data_ptr(), self.log_capacity,
+                self.progress.data_ptr(), _stream()), "mpc_fulltree_episodes_run")
+            left -= n
 
     read_progress = DeviceEpisodes.read_progress   # (calls, stop, leaves) per robot
     read_logs = DeviceEpisodes.read_logs

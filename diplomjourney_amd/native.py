@@ -18,8 +18,6 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_NAME = "libmpc_rollout.so"
 LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
-# Developer override for A/B-testing kernel variants built elsewhere.
-_LIB_OVERRIDE = os.environ.get("DIPLOMJOURNEY_MPC_LIB")
 SRC = os.path.join(PKG_DIR, "csrc", "mpc_rollout.hip")
 HEADER = os.path.join(REPO_DIR, "include", "mpc_rollout.h")
 
@@ -42,7 +40,7 @@ EXPORTS = (
     "mpc_episode_exchange_step2", "mpc_episode_exchange_mark",
     "mpc_stream_create_cu_reserved", "mpc_stream_create_cu_share", "mpc_stream_destroy",
     "mpc_mailbox_bytes", "mpc_mailbox_alloc", "mpc_mailbox_free", "mpc_mailbox_set_peers",
-    "mpc_mailbox_ping",
+    "mpc_mailbox_ping", "mpc_mailbox_clear",
     "mpc_ipc_handle",
     "mpc_ipc_open", "mpc_ipc_close", "mpc_peer_enable", "mpc_episode_p2p_step",
     "mpc_episode_p2p_flush",
@@ -108,7 +106,7 @@ def lib():
     if _lib is not None:
         return _lib
     import torch  # noqa: F401  (one HIP runtime: torch's libamdhip64.so.7)
-    path = _LIB_OVERRIDE or LIB_PATH
+    path = LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError(f"{path} is missing: run __graft_entry__.build() "
                            "(the MPC expansion has no CPU fallback)")
@@ -135,12 +133,11 @@ def lib():
                                              ctypes.c_size_t, _P, _P]
     L.mpc_stream_probe.restype = ctypes.c_int
     L.mpc_stream_probe.argtypes = [_P, _P, _I64, _I32, _P, ctypes.c_size_t, _P]
-    if not (_LIB_OVERRIDE and not hasattr(L, "mpc_stream_probe_tiled")):
-        L.mpc_stream_probe_tiled.restype = ctypes.c_int
-        L.mpc_stream_probe_tiled.argtypes = [_P, _I64, _I32, _P, ctypes.c_size_t, _P]
-        L.mpc_sample_controls_tiled.restype = ctypes.c_int
-        L.mpc_sample_controls_tiled.argtypes = [_P, _I32, _P, _I32, _I64, _I32, ctypes.c_uint64,
-                                                _I64, _I32, _P, _P]
+    L.mpc_stream_probe_tiled.restype = ctypes.c_int
+    L.mpc_stream_probe_tiled.argtypes = [_P, _I64, _I32, _P, ctypes.c_size_t, _P]
+    L.mpc_sample_controls_tiled.restype = ctypes.c_int
+    L.mpc_sample_controls_tiled.argtypes = [_P, _I32, _P, _I32, _I64, _I32, ctypes.c_uint64,
+                                            _I64, _I32, _P, _P]
     L.mpc_rcp_estimate.restype = ctypes.c_int
     L.mpc_rcp_estimate.argtypes = [_P, _P, _I64, _P]
     L.mpc_select_winner.restype = ctypes.c_int
@@ -189,19 +186,18 @@ def lib():
     L.mpc_episode_exchange_step.argtypes = [ctypes.POINTER(MpcEpisodeConfig), _P, ctypes.c_uint32,
                                             _P, _P, _I64, _I32, _I64, _I32, _P, ctypes.c_size_t,
                                             _P, _I32, _P, _P, _P, _I32, _P]
-    if not (_LIB_OVERRIDE and not hasattr(L, "mpc_episode_exchange_step2")):
-        L.mpc_episode_exchange_step2.restype = ctypes.c_int
-        L.mpc_episode_exchange_step2.argtypes = [
-            ctypes.POINTER(MpcEpisodeConfig), _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _I64,
-            _I32, _I64, _I32, _P, ctypes.c_size_t, _P, _I32, _P, _P, _P, _I32, _P]
-        L.mpc_episode_exchange_mark.restype = ctypes.c_int
-        L.mpc_episode_exchange_mark.argtypes = [_P, ctypes.c_uint32, _P]
-        L.mpc_stream_create_cu_reserved.restype = ctypes.c_int
-        L.mpc_stream_create_cu_reserved.argtypes = [_I32, ctypes.POINTER(_P)]
-        L.mpc_stream_create_cu_share.restype = ctypes.c_int
-        L.mpc_stream_create_cu_share.argtypes = [_I32, _I32, ctypes.POINTER(_P)]
-        L.mpc_stream_destroy.restype = ctypes.c_int
-        L.mpc_stream_destroy.argtypes = [_P]
+    L.mpc_episode_exchange_step2.restype = ctypes.c_int
+    L.mpc_episode_exchange_step2.argtypes = [
+        ctypes.POINTER(MpcEpisodeConfig), _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _I64,
+        _I32, _I64, _I32, _P, ctypes.c_size_t, _P, _I32, _P, _P, _P, _I32, _P]
+    L.mpc_episode_exchange_mark.restype = ctypes.c_int
+    L.mpc_episode_exchange_mark.argtypes = [_P, ctypes.c_uint32, _P]
+    L.mpc_stream_create_cu_reserved.restype = ctypes.c_int
+    L.mpc_stream_create_cu_reserved.argtypes = [_I32, ctypes.POINTER(_P)]
+    L.mpc_stream_create_cu_share.restype = ctypes.c_int
+    L.mpc_stream_create_cu_share.argtypes = [_I32, _I32, ctypes.POINTER(_P)]
+    L.mpc_stream_destroy.restype = ctypes.c_int
+    L.mpc_stream_destroy.argtypes = [_P]
     L.mpc_episode_exchange_flush.restype = ctypes.c_int
     L.mpc_episode_exchange_flush.argtypes = [ctypes.POINTER(MpcEpisodeConfig), _P, _I32, _P, _I32,
                                              _P, _P, _I32, _P]
@@ -215,49 +211,48 @@ def lib():
     L.mpc_episode_rollout.restype = ctypes.c_int
     L.mpc_episode_rollout.argtypes = [_P, _P, _P, _I64, _I32, _I64, _I32, _P, ctypes.c_size_t,
                                       _P, ctypes.POINTER(MpcEpisodeConfig), _P, _I32, _P]
-    if not (_LIB_OVERRIDE and not hasattr(L, "mpc_episode_p2p_step")):
-        L.mpc_mailbox_bytes.restype = ctypes.c_size_t
-        L.mpc_mailbox_bytes.argtypes = [_I32]
-        L.mpc_mailbox_alloc.restype = ctypes.c_int
-        L.mpc_mailbox_alloc.argtypes = [_I32, _I32, ctypes.POINTER(_P)]
-        L.mpc_mailbox_free.restype = ctypes.c_int
-        L.mpc_mailbox_free.argtypes = [_P]
-        L.mpc_ipc_handle.restype = ctypes.c_int
-        L.mpc_ipc_handle.argtypes = [_P, _P]
-        L.mpc_ipc_open.restype = ctypes.c_int
-        L.mpc_ipc_open.argtypes = [_P, ctypes.POINTER(_P)]
-        L.mpc_ipc_close.restype = ctypes.c_int
-        L.mpc_ipc_close.argtypes = [_P]
-        L.mpc_peer_enable.restype = ctypes.c_int
-        L.mpc_peer_enable.argtypes = [_I32]
-        L.mpc_mailbox_ping.restype = ctypes.c_int
-        L.mpc_mailbox_ping.argtypes = [_P, ctypes.c_uint32, _P, _P]
-        L.mpc_mailbox_set_peers.restype = ctypes.c_int
-        L.mpc_mailbox_set_peers.argtypes = [_P, _I32, _I32, ctypes.POINTER(_P)]
-        L.mpc_episode_p2p_step.restype = ctypes.c_int
-        L.mpc_episode_p2p_step.argtypes = [
-            ctypes.POINTER(MpcEpisodeConfig), _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _I64,
-            _I32, _I64, _I32, _P, _P, ctypes.c_size_t, _P, _P, _P, _I32, _P, _P, _I32, _P]
-        L.mpc_episode_p2p_flush.restype = ctypes.c_int
-        L.mpc_episode_p2p_flush.argtypes = [
-            ctypes.POINTER(MpcEpisodeConfig), _P, ctypes.c_uint32, _P, _P, _I64, _I32, _I64,
-            _I32, _P, ctypes.c_size_t, _P, _I32, _P, _P, _I32, _P]
-    if not (_LIB_OVERRIDE and not hasattr(L, "mpc_episodes_run")):   # (older A/B builds)
-        L.mpc_episodes_state_bytes.restype = ctypes.c_size_t
-        L.mpc_episodes_state_bytes.argtypes = [_I32]
-        L.mpc_episodes_reset.restype = ctypes.c_int
-        L.mpc_episodes_reset.argtypes = [_P, _I32, _P, _P]
-        L.mpc_episodes_run.restype = ctypes.c_int
-        L.mpc_episodes_run.argtypes = [_P, _I32, _I32, _I32, _I32, _P, _I32, _P, _P]
-    if not (_LIB_OVERRIDE and not hasattr(L, "mpc_fulltree_episodes_run")):
-        L.mpc_fulltree_episodes_state_bytes.restype = ctypes.c_size_t
-        L.mpc_fulltree_episodes_state_bytes.argtypes = [_I32]
-        L.mpc_fulltree_episodes_reset.restype = ctypes.c_int
-        L.mpc_fulltree_episodes_reset.argtypes = [_P, _I32, _P, _P]
-        L.mpc_fulltree_episodes_run.restype = ctypes.c_int
-        L.mpc_fulltree_episodes_run.argtypes = [
-            _P, _I32, _P, _I32, _P, _I32, ctypes.c_double, ctypes.c_double, ctypes.c_double,
-            _I32, _I32, _P, _I32, _P, _P]
+    L.mpc_mailbox_bytes.restype = ctypes.c_size_t
+    L.mpc_mailbox_bytes.argtypes = [_I32]
+    L.mpc_mailbox_alloc.restype = ctypes.c_int
+    L.mpc_mailbox_alloc.argtypes = [_I32, _I32, ctypes.POINTER(_P)]
+    L.mpc_mailbox_free.restype = ctypes.c_int
+    L.mpc_mailbox_free.argtypes = [_P]
+    L.mpc_ipc_handle.restype = ctypes.c_int
+    L.mpc_ipc_handle.argtypes = [_P, _P]
+    L.mpc_ipc_open.restype = ctypes.c_int
+    L.mpc_ipc_open.argtypes = [_P, ctypes.POINTER(_P)]
+    L.mpc_ipc_close.restype = ctypes.c_int
+    L.mpc_ipc_close.argtypes = [_P]
+    L.mpc_peer_enable.restype = ctypes.c_int
+    L.mpc_peer_enable.argtypes = [_I32]
+    L.mpc_mailbox_ping.restype = ctypes.c_int
+    L.mpc_mailbox_ping.argtypes = [_P, ctypes.c_uint32, _P, _P]
+    L.mpc_mailbox_clear.restype = ctypes.c_int
+    L.mpc_mailbox_clear.argtypes = [_P, _I32, _P]
+    L.mpc_mailbox_set_peers.restype = ctypes.c_int
+    L.mpc_mailbox_set_peers.argtypes = [_P, _I32, _I32, ctypes.POINTER(_P)]
+    L.mpc_episode_p2p_step.restype = ctypes.c_int
+    L.mpc_episode_p2p_step.argtypes = [
+        ctypes.POINTER(MpcEpisodeConfig), _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _I64,
+        _I32, _I64, _I32, _P, _P, ctypes.c_size_t, _P, _P, _P, _I32, _P, _P, _I32, _P]
+    L.mpc_episode_p2p_flush.restype = ctypes.c_int
+    L.mpc_episode_p2p_flush.argtypes = [
+        ctypes.POINTER(MpcEpisodeConfig), _P, ctypes.c_uint32, _P, _P, _I64, _I32, _I64,
+        _I32, _P, ctypes.c_size_t, _P, _I32, _P, _P, _I32, _P]
+    L.mpc_episodes_state_bytes.restype = ctypes.c_size_t
+    L.mpc_episodes_state_bytes.argtypes = [_I32]
+    L.mpc_episodes_reset.restype = ctypes.c_int
+    L.mpc_episodes_reset.argtypes = [_P, _I32, _P, _P]
+    L.mpc_episodes_run.restype = ctypes.c_int
+    L.mpc_episodes_run.argtypes = [_P, _I32, _I32, _I32, _I32, _P, _I32, _P, _P]
+    L.mpc_fulltree_episodes_state_bytes.restype = ctypes.c_size_t
+    L.mpc_fulltree_episodes_state_bytes.argtypes = [_I32]
+    L.mpc_fulltree_episodes_reset.restype = ctypes.c_int
+    L.mpc_fulltree_episodes_reset.argtypes = [_P, _I32, _P, _P]
+    L.mpc_fulltree_episodes_run.restype = ctypes.c_int
+    L.mpc_fulltree_episodes_run.argtypes = [
+        _P, _I32, _P, _I32, _P, _I32, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+        _I32, _I32, _P, _I32, _P, _P]
     _lib = L
     return L
 

@@ -455,6 +455,11 @@ int mpc_mailbox_set_peers(void* mailbox, int32_t rank, int32_t world, const void
  * waits (~0.1 s at most) for all of its own; *ok (device int32) = 1 if all
  * arrived.  A host that gets 0 on any rank uses the all_gather exchange. */
 int mpc_mailbox_ping(void* mailbox, uint32_t tag, int32_t* ok, mpc_stream_t stream);
+/* Zero this rank's candidate slots (not the header) on `stream`: with the
+ * episode's reset, so that a step replayed with an epoch of an earlier run
+ * (a HIP graph captured before the reset) never reads a stale granule whose
+ * tag matches.  Call it while no peer stores into this mailbox. */
+int mpc_mailbox_clear(void* mailbox, int32_t world, mpc_stream_t stream);
 int mpc_ipc_handle(void* dev_ptr, void* handle /* MPC_IPC_HANDLE_BYTES */);
 int mpc_ipc_open(const void* handle, void** dev_ptr);
 int mpc_ipc_close(void* dev_ptr);

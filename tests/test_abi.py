@@ -146,7 +146,7 @@ def test_argument_validation_without_gpu():
 def test_no_cpu_fallback(monkeypatch, tmp_path):
     """The product binding raises when the HIP library is absent."""
     monkeypatch.setattr(native, "_lib", None)
-    monkeypatch.setattr(native, "_LIB_OVERRIDE", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(native, "LIB_PATH", str(tmp_path / "missing.so"))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         native.lib()
 

@@ -1302,12 +1302,23 @@ def test_bench_contract(extra):
         assert d["config"]["step_launches"].startswith("chained")
         ro = d["roofline_rollout_only"]
         assert ro["kernel"] == "k_rollout_argmin_stream" and 0 < ro["frac"] < 1
-        # the reference arithmetic's winner on every parity step (oracle qk21)
-        assert d["parity"]["identity_rate"] == 1.0 and d["parity"]["steps"] == 8, d["parity"]
+        # every checker leg against the reference arithmetic (oracle qk21):
+        # the episode through the reference's events and a restart, the
+        # samplers, the S1 = 451 full tree, the device episode drivers
+        par = d["parity"]
+        assert par["pass"] and all(par["checks"].values()), par["checks"]
+        assert par["steps"] == 116 and par["identity_rate"] == 1.0, par
+        assert par["episode"]["events_at_p"] == [60, 90, 110] and par["episode"]["restarts"] >= 1
+        assert par["max_abs_pose_diff"] <= 1e-9
         cd = d["config_d"]      # BASELINE config D's one-GPU share in the same run
         assert cd["chain_error"] == 0 and cd["config"]["candidates_per_gpu"] == 1_250_000
         assert cd["roofline"]["kernel"] == "k_episode_chain"
         assert cd["roofline"]["algorithmic_bytes_per_launch"] == 16.0 * 12 * 1_250_000
+        ct = d["config_d_total"]   # config D as written: 1e7 in total (all on one GPU)
+        assert ct["chain_error"] == 0 and ct["config"]["candidates_total"] == 10_000_000
+        assert ct["roofline"]["algorithmic_bytes_per_launch"] == 16.0 * 12 * 10_000_000
+        assert ct["scaling"] == "strong" and 0 < ct["roofline"]["frac"] < 1
+        assert d["ramp"]["steps"] >= 300
     assert rf["traffic"] is not None and abs(rf["traffic"] / 160e6 - 1) < 0.01
 
 
@@ -1347,8 +1358,15 @@ def test_bench_two_ranks_spawned(mode):
     assert rf["algorithmic_bytes_per_launch"] == 16.0 * 10 * 100_000
     # the sampled second pass (expand + advance: the 808-B all_gather) ran
     assert d["other_inputs"]["inputs"] == "sampled" and d["other_inputs"]["value"] > 0
-    # every parity step's winner is the reference arithmetic's (oracle qk21)
-    assert d["parity"]["identity_rate"] == 1.0, d["parity"]
+    # every checker leg against the reference arithmetic (oracle qk21), the
+    # episode leg with the N > 1 schedule (events at p = 6 / 12 / 16, a restart)
+    assert d["parity"]["pass"] and d["parity"]["identity_rate"] == 1.0, d["parity"]["checks"]
+    assert d["parity"]["episode"]["events_at_p"] == [6, 12, 16]
+    # config D as written: 1e7 candidates in total over the two ranks
+    ct = d["config_d_total"]
+    assert ct["chain_error"] == 0 and ct["value"] > 0
+    assert ct["config"]["candidates_total"] == 10_000_000
+    assert ct["config"]["candidates_per_gpu"] == 5_000_000
     # BASELINE config D in the same run: N=12, 1.25e6 per GPU, same step form
     cd = d["config_d"]
     assert cd["chain_error"] == 0 and cd["value"] > 0

@@ -205,6 +205,6 @@ def test_bench_spawned_rank_failure_fails_the_run():
                {"WORLD_SIZE": "2"}, drop=("RANK", "LOCAL_RANK"))
     assert r.returncode == 0          # under a launcher: WORLD_SIZE matches, no spawn
     r = _bench(["--gpus", "2", "--dist-backend", "gloo", "--workload", "C", "--steps", "4",
-                "--cpu-seconds", "0"], {"DIPLOMJOURNEY_MPC_LIB": "/nonexistent/lib.so"})
+                "--cpu-seconds", "0"], {"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": ""})
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

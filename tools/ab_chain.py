@@ -1,5 +1,5 @@
 """Same-box A/B of library builds at config C: for each library (env
-DIPLOMJOURNEY_MPC_LIB=<path>, one child process per measurement, interleaved
+tools/with_lib.py <path>, one child process per measurement, interleaved
 for R rounds) the chained launch and the plain streaming kernel, 300 warm +
 200 timed back-to-back launches between HIP events over 8 resident batches.
     python tools/ab_chain.py ROUNDS LIB [LIB ...]      (LIB "-" = in-tree build)"""
@@ -60,9 +60,11 @@ def main():
     for _ in range(rounds):
         for lib in libs:
             env = dict(os.environ)
+            cmd = [sys.executable, os.path.abspath(__file__), "--child"]
             if lib != "-":
-                env["DIPLOMJOURNEY_MPC_LIB"] = os.path.abspath(lib)
-            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child"], env=env,
+                cmd = [sys.executable, os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                    "with_lib.py"), os.path.abspath(lib)] + cmd[1:]
+            r = subprocess.run(cmd, env=env,
                                capture_output=True, text=True, timeout=300)
             line = [ln for ln in r.stdout.splitlines() if ln.startswith("AB ")]
             if r.returncode != 0 or not line:

@@ -148,8 +148,9 @@ B0_P2P = {1: "candidate", 2: "posted", 3: "gathered", 6: "advance", 8: "publishe
 
 
 def run(n, ns, mode="chain"):
-    os.environ["DIPLOMJOURNEY_MPC_LIB"] = VAR
     sys.path.insert(0, REPO)
+    from diplomjourney_amd import native
+    native.LIB_PATH = VAR            # the timeline build (developer tool)
     import torch
     from diplomjourney_amd import math_model_tree as mmt
     from diplomjourney_amd import native
