@@ -211,9 +211,11 @@ __device__ inline void episode_grids(const mpc_episode_config_t& c, const Episod
     const uint64_t m = __ballot(ok);
     const int pos = nv + __popcll(m & below);
     if (ok && pos < kEpMaxGrid) s_v[pos] = cand;
-    double mn = ok ? cand : __builtin_inf();
-    for (int off = 32; off > 0; off >>= 1) mn = fmin(mn, __shfl_xor(mn, off, 64));
-    vmin = fmin(vmin, mn);
+    if (S.steps_for_slowing > 0) {   // (uniform) min(V) only for the slow-down
+      double mn = ok ? cand : __builtin_inf();
+      for (int off = 32; off > 0; off >>= 1) mn = fmin(mn, __shfl_xor(mn, off, 64));
+      vmin = fmin(vmin, mn);
+    }
     nv += __popcll(m);
   }
   nv = nv < kEpMaxGrid ? nv : kEpMaxGrid;

@@ -96,16 +96,79 @@ __device__ __forceinline__ double const_candidate_cost(const Consts& K, double v
                   : const_candidate_cost_l<INTEG, ROT, false>(K, v, b, n_steps);
 }
 
+// Two candidates' recurrences in one loop — independent chains the scheduler
+// interleaves — each with exactly const_candidate_cost_l's operations (the
+// same bits per candidate).
+// NS > 0: the horizon as a compile-time constant (the reference's N = 3):
+// the loop unrolls, and the steps' sin/cos — which depend only on the heading
+// chain, a sum of the candidate's constant increment — overlap.
+template <int INTEG, int ROT, bool PL2, int NS = 0>
+__device__ __forceinline__ void const_pair_cost_l(const Consts& K, const double (&v)[2],
+                                                  const double (&b)[2], int n_steps,
+                                                  double (&cst)[2]) {
+  if constexpr (NS > 0) n_steps = NS;
+  double x[2], y[2], ph[2], s[2], c[2];
+  bool bad[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    step_start<ROT>(K, x[j], y[j], ph[j], s[j], c[j]);
+    bad[j] = false;
+  }
+  auto one_step = [&]() {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      step_core<INTEG, ROT, PL2>(x[j], y[j], ph[j], s[j], c[j], v[j], b[j], K, bad[j]);
+  };
+  if constexpr (NS > 0) {
+#pragma unroll
+    for (int st = 0; st < NS; ++st) one_step();
+  } else {
+    for (int st = 0; st < n_steps; ++st) one_step();
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if constexpr (ROT == kRotCum) {
+      if (!bad[j]) cum_pose<PL2>(K, x[j], y[j], x[j], y[j]);
+    }
+    if (bad[j]) {
+      x[j] = K.x;
+      y[j] = K.y;
+      ph[j] = K.phi;
+      for (int st = 0; st < n_steps; ++st) step_safe<INTEG>(x[j], y[j], ph[j], v[j], b[j], K);
+    }
+    cst[j] = cost(x[j], y[j], K);
+  }
+}
+
+template <int INTEG, int ROT, int NS = 0>
+__device__ __forceinline__ void const_pair_cost(const Consts& K, const double (&v)[2],
+                                                const double (&b)[2], int n_steps,
+                                                double (&cst)[2]) {
+  if (K.L_pow2)
+    const_pair_cost_l<INTEG, ROT, true, NS>(K, v, b, n_steps, cst);
+  else
+    const_pair_cost_l<INTEG, ROT, false, NS>(K, v, b, n_steps, cst);
+}
+
 // Block r = robot r: up to max_calls MPC steps of its episode (fewer if it
 // ends).  log: [n][cap] ring per robot; progress (optional): {calls, stop,
 // candidates} per robot after the launch.
-// 4 waves per SIMD (<= 128 VGPRs): 4 robots per CU at a time.
+// NT = 256: 4 waves per SIMD (<= 128 VGPRs), 4 robots per CU at a time; a
+// robot's serial phases (grid, re-roll, update: one lane) then share their
+// SIMD with three other robots' waves.
+// NT = 64 (the default for N <= 21): ONE wave per robot — 1000 robots are
+// ~1 wave per SIMD, so the serial phases run uncontended; a lane rolls out
+// its candidates two at a time (const_pair_cost), the arg-min is one DPP
+// wave reduction and the barriers are a single wave's.
+// PAIR: a lane's candidates two at a time, interleaved (const_pair_cost);
+// else one after the other (more waves per SIMD fit: <= 128 VGPRs).
 constexpr int kEpisodesWaves = 4;
-template <int INTEG, int ROT>
-__global__ __launch_bounds__(kBlock, kEpisodesWaves) void k_episodes_run(
+template <int INTEG, int ROT, int NT = kBlock, bool PAIR = (NT == 64)>
+__global__ __launch_bounds__(NT, PAIR ? 2 : kEpisodesWaves) void k_episodes_run(
     const mpc_episode_config_t* __restrict__ cfgs, RobotState* __restrict__ robots, int n_steps,
     int max_calls, mpc_episode_log_t* __restrict__ log, int cap,
     mpc_episodes_progress_t* __restrict__ progress) {
+  static_assert(NT == 64 || NT == kBlock, "one wave or one standard block per robot");
   const int r = blockIdx.x;
   const mpc_episode_config_t& c = cfgs[r];
   RobotState* __restrict__ R = &robots[r];
@@ -117,8 +180,8 @@ __global__ __launch_bounds__(kBlock, kEpisodesWaves) void k_episodes_run(
   __shared__ mpc_episode_log_t s_log;
   __shared__ mpc_result_t s_out;
   __shared__ EmitLds lds;
-  if (threadIdx.x < kStoredWords)
-    s_head[threadIdx.x] = reinterpret_cast<const uint64_t*>(R)[threadIdx.x];
+  for (int q = threadIdx.x; q < kStoredWords; q += NT)
+    s_head[q] = reinterpret_cast<const uint64_t*>(R)[q];
   if (threadIdx.x == 0) {
     s_stop = R->stop;
     s_calls = R->calls;
@@ -142,21 +205,51 @@ __global__ __launch_bounds__(kBlock, kEpisodesWaves) void k_episodes_run(
     const int nv = s_nv, nb = s_nb, n_grid = nv * nb;
     uint64_t best_k = ~0ull;
     int64_t best_i = INT64_MAX;
-    for (int k0 = 2 * threadIdx.x; k0 < n_grid; k0 += 2 * kBlock) {
+    if constexpr (PAIR) {
+      // lane l: candidates l, l + NT, l + 2 NT, ... two per pass (ascending per
+      // lane: strict < keeps the first)
+      for (int k0 = threadIdx.x; k0 < n_grid; k0 += 2 * NT) {
+        const int k1 = k0 + NT;
+        const bool has1 = k1 < n_grid;
+        const int kq = has1 ? k1 : k0;   // (a valid stand-in; its cost is not used)
+        const double vv[2] = {s_v[k0 / nb], s_v[kq / nb]};
+        const double bb[2] = {s_b[k0 % nb], s_b[kq % nb]};
+        double cst[2];
+        if (n_steps == 3)   // uniform: the reference's horizon, unrolled
+          const_pair_cost<INTEG, ROT, 3>(K, vv, bb, n_steps, cst);
+        else
+          const_pair_cost<INTEG, ROT>(K, vv, bb, n_steps, cst);
+        uint64_t kk = cost_key_nonneg(cst[0]);
+        if (kk < best_k) {
+          best_k = kk;
+          best_i = k0;
+        }
+        kk = cost_key_nonneg(cst[1]);
+        if (has1 && kk < best_k) {
+          best_k = kk;
+          best_i = k1;
+        }
+      }
+    } else {
+      for (int k0 = 2 * threadIdx.x; k0 < n_grid; k0 += 2 * kBlock) {
 #pragma unroll 1
-      for (int j = 0; j < 2; ++j) {
-        const int k = k0 + j;   // ascending per lane: strict < keeps the first
-        if (k < n_grid) {
-          const uint64_t kk = cost_key_nonneg(
-              const_candidate_cost<INTEG, ROT>(K, s_v[k / nb], s_b[k % nb], n_steps));
-          if (kk < best_k) {
-            best_k = kk;
-            best_i = k;
+        for (int j = 0; j < 2; ++j) {
+          const int k = k0 + j;   // ascending per lane: strict < keeps the first
+          if (k < n_grid) {
+            const uint64_t kk = cost_key_nonneg(
+                const_candidate_cost<INTEG, ROT>(K, s_v[k / nb], s_b[k % nb], n_steps));
+            if (kk < best_k) {
+              best_k = kk;
+              best_i = k;
+            }
           }
         }
       }
     }
-    block_argmin<true>(best_k, best_i);
+    if constexpr (NT == 64)
+      wave_argmin32(best_k, best_i);   // (every lane holds the minimum)
+    else
+      block_argmin<true>(best_k, best_i);
     if (threadIdx.x == 0) {
       s_bk = best_k;
       s_bi = best_i;
@@ -191,7 +284,7 @@ __global__ __launch_bounds__(kBlock, kEpisodesWaves) void k_episodes_run(
           [threadIdx.x] = reinterpret_cast<const uint64_t*>(&s_log)[threadIdx.x];
   }
   __syncthreads();
-  if (threadIdx.x < kStoredWords) reinterpret_cast<uint64_t*>(R)[threadIdx.x] = s_head[threadIdx.x];
+  for (int q = threadIdx.x; q < kStoredWords; q += NT) reinterpret_cast<uint64_t*>(R)[q] = s_head[q];
   if (threadIdx.x == 0) {
     R->stop = s_stop;
     R->calls = s_calls;

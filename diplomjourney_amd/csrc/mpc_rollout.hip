@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <type_traits>
 
 #include "../../include/mpc_rollout.h"
@@ -1044,15 +1045,31 @@ int mpc_exchange_allgather_group(int32_t n, const mpc_comm_t* comms,
   return st;
 }
 
+// One word device -> coherent pinned host memory by a one-lane kernel (a
+// vector store over the fabric), not by an async memory copy: a 4-B
+// hipMemcpyAsync to pageable memory on a CU-masked stream (the overlapped
+// exchange's launch stream) left its completion callback undelivered at
+// process exit under rocprofv3's memory-copy tracing (profiles/r06/overlap_exit/).
+__global__ void k_read_word(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst) {
+  if (threadIdx.x == 0) *dst = *src;
+}
+
 int mpc_episode_chain_error(const void* state, int32_t* error, mpc_stream_t stream) {
   if (!state || !error) return MPC_ERR_ARG;
-  uint32_t e = 0;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (hipMemcpyAsync(&e, &static_cast<const EpisodeState*>(state)->chain_error, sizeof(e),
-                     hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
+  static std::mutex mu;
+  static uint32_t* host = nullptr;   // process lifetime
+  std::lock_guard<std::mutex> lock(mu);
+  if (!host && hipHostMalloc(reinterpret_cast<void**>(&host), 256, hipHostMallocCoherent) !=
+                   hipSuccess) {
+    host = nullptr;
     return MPC_ERR_HIP;
-  *error = static_cast<int32_t>(e);
+  }
+  *reinterpret_cast<volatile uint32_t*>(host) = ~0u;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  k_read_word<<<1, 64, 0, st>>>(&static_cast<const EpisodeState*>(state)->chain_error, host);
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+    return MPC_ERR_HIP;
+  *error = static_cast<int32_t>(*reinterpret_cast<volatile uint32_t*>(host));
   return MPC_OK;
 }
 
@@ -1113,12 +1130,29 @@ int mpc_episodes_run(void* state, int32_t n_robots, int32_t n_steps, int32_t int
   char* s = static_cast<char*>(state);
   const mpc_episode_config_t* dcfg =
       reinterpret_cast<const mpc_episode_config_t*>(s + episodes_cfg_offset(n_robots));
+#ifndef MPC_EP_VARIANT
+#define MPC_EP_VARIANT 2
+#endif
+  // 0: one 256-thread block per robot, a lane's two candidates in turn;
+  // 1: one wave per robot, its candidates two at a time (while the winner's
+  //    trajectory fits one value per lane: emit_winner's store);
+  // 2: one 256-thread block per robot, a lane's two candidates interleaved
+  const int variant = (MPC_EP_VARIANT == 1 && 3 * n_steps > 64) ? 2 : MPC_EP_VARIANT;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  RobotState* robots = reinterpret_cast<RobotState*>(s);
+  const int cap = log ? log_capacity : 0;
   dispatch_mode(integrator, [&](auto integ, auto rot) {
     constexpr int I = decltype(integ)::value;
     constexpr int R = decltype(rot)::value;
-    k_episodes_run<I, R><<<n_robots, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
-        dcfg, reinterpret_cast<RobotState*>(s), n_steps, max_calls, log, log ? log_capacity : 0,
-        progress);
+    if (variant == 1)
+      k_episodes_run<I, R, 64, true><<<n_robots, 64, 0, st>>>(dcfg, robots, n_steps, max_calls,
+                                                               log, cap, progress);
+    else if (variant == 2)
+      k_episodes_run<I, R, kBlock, true><<<n_robots, kBlock, 0, st>>>(
+          dcfg, robots, n_steps, max_calls, log, cap, progress);
+    else
+      k_episodes_run<I, R, kBlock, false><<<n_robots, kBlock, 0, st>>>(
+          dcfg, robots, n_steps, max_calls, log, cap, progress);
   });
   return last_hip_status();
 }

@@ -824,7 +824,15 @@ class DeviceEpisode:
         err = self.chain_error()
         if err:
             raise ChainError(err)
-        raw = self.log.cpu().numpy().tobytes()
+        # the log is complete: one copy into pinned host memory (a staged copy
+        # to pageable memory left an async-copy completion callback undelivered
+        # at process exit under rocprofv3's memory-copy tracing,
+        # profiles/r06/overlap_exit/)
+        if getattr(self, "_log_host", None) is None:
+            self._log_host = torch.empty(self.log.numel(), dtype=torch.uint8).pin_memory()
+        self._log_host.copy_(self.log, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        raw = self._log_host.numpy().tobytes()
         n = min(self.steps_enqueued, self.log_capacity)
         recs = [MpcEpisodeLog.from_buffer_copy(raw[i * LOG_BYTES:(i + 1) * LOG_BYTES])
                 for i in range(self.log_capacity)]
