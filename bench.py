@@ -85,8 +85,9 @@ WORKLOADS["R"] = dict(n_steps=3, per_gpu=None, robots=1000,
                            "block per robot (mpc_episodes_run)")
 WORKLOADS["G"] = dict(n_steps=3, per_gpu=None, robots=1000,
                       desc="run_math_model.py's 1000 episodes (SURVEY 8f 4): one robot per "
-                           "episode, lockstep, one batched full-tree launch per MPC step, "
-                           "S1 = 5 x 13 controls (274,625 leaves per robot-step)")
+                           "episode, device-resident lockstep over the robots still running "
+                           "(each call's leaves spread over the whole GPU), S1 = 5 x 13 "
+                           "controls (274,625 leaves per robot-step)")
 FP64_VECTOR_PEAK_TFLOPS = 78.6   # MI355X spec (2 x 32 lanes x 2 flops/clk/SIMD at 2.4 GHz / 2)
 # fp64 operations per full-tree leaf (csrc/mpc_fulltree.h, one layer step + criterion), as
 # written (an fma = 2): rect+rot 29 (heading add 1, rotation 6, two fused position updates 4,
@@ -1379,7 +1380,7 @@ VALU_JSON = {("k_episode_chain", "rect+cum"): ("r05/valu/chain.json", 1_000_000,
              # the device-resident episode drivers: the whole run is ONE launch;
              # keyed (episodes, max_calls) of workloads R and G as the bench runs them
              ("k_episodes_run", "qk21"): ("r05/valu/episodes_R.json", 1000, 1000),
-             ("k_ft_episodes_run", "rect+rot"): ("r05/valu/ftepisodes_G.json", 1000, 50)}
+             ("k_ftl_", "rect+rot"): ("r06/valu/ftepisodes_G.json", 1000, 50)}
 
 
 def valu_roofline(kernel, integrator, ms, n_cand, n_steps, note=None):
@@ -1720,8 +1721,10 @@ def bench_tree_episodes(args, wl, eng, rank, world, cpu):
 def bench_episodes(args, wl, eng, rank, world, cpu):
     """Config G: the script's episode loop for 1000 episodes at once (robots
     sharded over ranks, no exchange), device-resident (run_batched ->
-    mpc_fulltree_episodes_run: one block per robot runs its episode's
-    full-tree calls back to back in ONE launch).  Timed: up to K = --steps
+    mpc_fulltree_episodes_run, csrc/mpc_ftepisodes.h: per call three launches
+    over the robots still running — stop rules + compaction + the call's
+    control table, the leaves of every live robot spread over the whole GPU,
+    one update block per live robot; no host step).  Timed: up to K = --steps
     calls of every episode (K as max_calls) between syncs; ms_per_step = that
     time / the longest episode's calls (a lockstep-equivalent step)."""
     import math as _m
@@ -1776,18 +1779,19 @@ def bench_episodes(args, wl, eng, rank, world, cpu):
         "config": {"workload": wl["desc"], "s1": s1, "robots": wl["robots"],
                    "robot_steps": robot_steps, "lockstep_steps": lockstep,
                    "integrator": args.integrator, "episode_stops_rank0": stops,
-                   "episode_loop": "device-resident: one block per robot, one launch for all "
-                                   "calls (mpc_fulltree_episodes_run)",
+                   "episode_loop": "device-resident lockstep over the live robots: per call "
+                                   "k_ftl_prepare + k_ftl_leaves (grid spread over the live "
+                                   "robots) + k_ftl_update (mpc_fulltree_episodes_run)",
                    "parallelism": f"robot-sharded x{world}, no exchange"},
         "p50_note": "ms_per_step = the run's time (one launch + sync) / the longest "
                     "episode's calls",
         "roofline": {"bound": "valu-fp64", "achieved": flops / 1e12,
                      "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": flops / 1e12 / FP64_VECTOR_PEAK_TFLOPS, "traffic": None,
-                     "kernel": "k_ft_episodes_run",
+                     "kernel": "k_ftl_leaves",
                      "note": "algorithmic fp64 ops per leaf as written (FT_FLOPS_PER_LEAF) x "
                              "the leaves scored, over the whole timed run"},
-        "roofline_valu": valu_roofline("k_ft_episodes_run", args.integrator, elapsed * 1e3,
+        "roofline_valu": valu_roofline("k_ftl_", args.integrator, elapsed * 1e3,
                                        wl["robots"], args.steps,
                                        note="counted fp64 ops of the whole run (PMC) over the "
                                             "timed run"),

@@ -1292,9 +1292,11 @@ int mpc_fulltree_argmin_batched(const mpc_fulltree_problem_t* problems,
 }
 
 // ----------------------------- full-tree episodes ----------------------------
+// The state: FtEpisode[R], the lockstep form's scratch (ftl_bytes), then the
+// R configurations (mpc_fulltree_episodes_reset copies them in).
 size_t mpc_fulltree_episodes_state_bytes(int32_t n_robots) {
   if (n_robots < 1) return 0;
-  return ft_align(static_cast<size_t>(n_robots) * sizeof(FtEpisode)) +
+  return ftl_bytes(n_robots) +
          static_cast<size_t>(n_robots) * sizeof(mpc_fulltree_episode_config_t);
 }
 
@@ -1305,8 +1307,7 @@ int mpc_fulltree_episodes_reset(const mpc_fulltree_episode_config_t* cfgs, int32
     if (cfgs[r].max_calls < 0) return MPC_ERR_ARG;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   char* s = static_cast<char*>(state);
-  auto* dcfg = reinterpret_cast<mpc_fulltree_episode_config_t*>(
-      s + ft_align(static_cast<size_t>(n_robots) * sizeof(FtEpisode)));
+  auto* dcfg = reinterpret_cast<mpc_fulltree_episode_config_t*>(s + ftl_bytes(n_robots));
   // (pageable host source: the copy has read it when the call returns)
   if (hipMemcpyAsync(dcfg, cfgs, static_cast<size_t>(n_robots) * sizeof(*cfgs),
                      hipMemcpyHostToDevice, st) != hipSuccess)
@@ -1328,13 +1329,46 @@ int mpc_fulltree_episodes_run(void* state, int32_t n_robots, const double* v_gri
   if (static_cast<int64_t>(n_v) * n_beta > kFtEpMaxS1) return MPC_ERR_UNSUPPORTED;
   if (mode_ok(integrator, false) != MPC_OK) return MPC_ERR_UNSUPPORTED;
   if (max_calls == 0) return MPC_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  FtEpisode* E = reinterpret_cast<FtEpisode*>(state);
+  const int cap = log ? log_capacity : 0;
+#ifndef MPC_FT_LOCKSTEP
+#define MPC_FT_LOCKSTEP 1
+#endif
+  if (!MPC_FT_LOCKSTEP) {   // one block per robot, every call in one launch
+    dispatch_mode2(integrator, [&](auto integ, auto rot) {
+      constexpr int I = decltype(integ)::value;
+      constexpr bool R = decltype(rot)::value;
+      k_ft_episodes_run<I, R><<<n_robots, kBlock, 0, st>>>(
+          E, v_grid, n_v, beta_grid, n_beta, L, delta_t, eps, max_calls, log, cap, progress);
+    });
+    return last_hip_status();
+  }
+  // load-balanced lockstep (mpc_ftepisodes.h): three launches per call over
+  // the robots still running, the leaves of each spread over `grid` blocks
+  char* s = static_cast<char*>(state);
+  auto* ls = reinterpret_cast<FtLockstep*>(s + ftl_ls_offset(n_robots));
+  auto* ctl = reinterpret_cast<FtCtl*>(s + ftl_ctl_offset(n_robots));
+  auto* live = reinterpret_cast<int32_t*>(s + ftl_live_offset(n_robots));
+  auto* robots = reinterpret_cast<FtRobot*>(s + ftl_robots_offset(n_robots));
+  auto* part = reinterpret_cast<Rec*>(s + ftl_part_offset(n_robots));
+  const int64_t s1 = static_cast<int64_t>(n_v) * n_beta;
+  const int grid = static_cast<int>(std::min<int64_t>(kFtlMaxGrid, device_cus() * kFtWaves));
   dispatch_mode2(integrator, [&](auto integ, auto rot) {
     constexpr int I = decltype(integ)::value;
     constexpr bool R = decltype(rot)::value;
-    k_ft_episodes_run<I, R><<<n_robots, kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
-        reinterpret_cast<FtEpisode*>(state), v_grid, n_v, beta_grid, n_beta, L, delta_t, eps,
-        max_calls, log, log ? log_capacity : 0, progress);
+    for (int call = 0; call < max_calls; ++call) {
+      k_ftl_prepare<I><<<1, kFtlPrepBlock, 0, st>>>(E, n_robots, v_grid, n_v, beta_grid, n_beta,
+                                                     L, delta_t, eps, grid, ls, ctl, live,
+                                                     robots);
+      k_ftl_leaves<I, R><<<grid, kBlock, 0, st>>>(ls, ctl, live, robots, s1, part);
+      k_ftl_update<I, R><<<n_robots, kBlock, 0, st>>>(E, ls, ctl, live, robots, part, s1,
+                                                      delta_t, log, cap);
+    }
   });
+  if (progress)
+    k_ftl_progress<<<static_cast<unsigned>(cdiv(n_robots, 256)), 256, 0, st>>>(E, n_robots,
+                                                                               progress);
   return last_hip_status();
 }
 

@@ -926,10 +926,12 @@ class DeviceEpisodes:
 
 class DeviceFtEpisodes:
     """R robots' run_math_model.py episodes with the script's own full-tree MPC
-    step, in HBM (mpc_fulltree_episodes_*, csrc/mpc_ftepisodes.h): one block per
-    robot runs its episode's calls back to back, `run(k)` is ONE launch of up
-    to k calls of every robot.  cfgs: MpcFulltreeEpisodeConfig per robot;
-    v_grid / beta_grid: the script's grids as device tensors."""
+    step, in HBM (mpc_fulltree_episodes_*, csrc/mpc_ftepisodes.h): `run(k)`
+    enqueues up to k calls of every robot with no host step in between — per
+    call the robots still running are compacted and every one's S1^3 leaves
+    are spread over the whole GPU (the load-balanced lockstep form).  cfgs:
+    MpcFulltreeEpisodeConfig per robot; v_grid / beta_grid: the script's grids
+    as device tensors."""
 
     def __init__(self, engine, cfgs, v_grid, beta_grid, L, delta_t, eps, integrator="qk21",
                  log_capacity=256):
@@ -955,26 +957,16 @@ class DeviceFtEpisodes:
                      "mpc_fulltree_episodes_reset")
         self.progress.zero_()
 
-    # leaves one block may score in one launch (a robot's calls x S1^3): ~1 s
-    # of qk21 arithmetic per block, far below the driver's compute-lockup
-    # timeout whatever S1 and max_calls the caller asks for
-    LEAF_BUDGET = 1 << 30
-
     def run(self, max_calls):
-        """Enqueue up to max_calls MPC calls of every still-running robot: as
-        few launches as LEAF_BUDGET allows (chunked launches continue the
-        episodes exactly as one launch would)."""
-        s1 = self.vg.numel() * self.bg.numel()
-        per = max(1, min(int(max_calls), self.LEAF_BUDGET // max(1, s1 ** 3)))
-        left = int(max_calls)
-        while left > 0:
-            n = min(per, left)
-            native.check(self.lib.mpc_fulltree_episodes_run(
-                self.state.data_ptr(), self.R, self.vg.data_ptr(), self.vg.numel(),
-                self.bg.data_ptr(), self.bg.numel(), self.L, self.delta_t, self.eps,
-                self._integ, n, self.log.data_ptr(), self.log_capacity,
-                self.progress.data_ptr(), _stream()), "mpc_fulltree_episodes_run")
-            left -= n
+        """Enqueue up to max_calls MPC calls of every still-running robot
+        (three launches per call, each bounded by one call's S1^3 leaves per
+        robot spread over the GPU: no launch approaches the compute-lockup
+        timeout whatever S1 and max_calls are)."""
+        native.check(self.lib.mpc_fulltree_episodes_run(
+            self.state.data_ptr(), self.R, self.vg.data_ptr(), self.vg.numel(),
+            self.bg.data_ptr(), self.bg.numel(), self.L, self.delta_t, self.eps, self._integ,
+            int(max_calls), self.log.data_ptr(), self.log_capacity, self.progress.data_ptr(),
+            _stream()), "mpc_fulltree_episodes_run")
 
     read_progress = DeviceEpisodes.read_progress   # (calls, stop, leaves) per robot
     read_logs = DeviceEpisodes.read_logs

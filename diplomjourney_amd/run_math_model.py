@@ -241,10 +241,11 @@ class _Robot:
 def run_batched(starts, max_calls=None, integrator=None, chunk=256, stats=None):
     """The script's episode loop (:231-280) for len(starts) episodes at once,
     device-resident (mpc_fulltree_episodes_run, csrc/mpc_ftepisodes.h): one
-    robot per episode, one block per robot runs its episode's full-tree MPC
-    steps back to back — the stop rules, t += delta_t, the S1^3 leaves against
-    the robot's never-reset incumbent, its stale winner, the two-non-move stop —
-    `chunk` calls per launch with no host step in between.  Returns
+    robot per episode; per call the robots still running are compacted and
+    each one's S1^3 leaves spread over the whole GPU — the stop rules, t +=
+    delta_t, the leaves against the robot's never-reset incumbent, its stale
+    winner, the two-non-move stop — `chunk` calls per host call with no host
+    step in between.  Returns
     [(records, stop)] per episode, as run_episode does (records rebuilt from
     the per-step log: pre = (x, y, phi, v, t, optimal_criterion) before the
     call, ret, optimal_criterion after it); raises the script's TypeError if an

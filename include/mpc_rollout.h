@@ -621,10 +621,14 @@ int mpc_fulltree_argmin_batched(const mpc_fulltree_problem_t* problems,
 /* ---------------------------------------------------------------------------
  * Full-tree episodes, device-resident: run_math_model.py's
  * episode loop (:231-280) with its OWN full-tree MPC step (:133-228, the tree
- * of mpc_fulltree_argmin) for R robots, one robot per episode.  ONE launch
- * runs up to max_calls MPC steps of every robot (one block per robot, per-robot
- * state in HBM, no host round trip, no lockstep): the stop rules before each
- * call (on target :261, the robot's max_calls), t += delta_t (:156), the S1^3
+ * of mpc_fulltree_argmin) for R robots, one robot per episode.  ONE call
+ * enqueues up to max_calls MPC steps of every robot (per-robot state in HBM,
+ * no host round trip): per MPC step three launches over the robots still
+ * running — compaction and the step's control table, every live robot's
+ * leaves spread over the whole GPU, one update per live robot (live robots
+ * have run the same number of calls: one quad window, one table).  Per call:
+ * the stop rules before it (on target :261, the robot's max_calls), t +=
+ * delta_t (:156), the S1^3
  * leaves scored with the heading-term criterion, strict < against the robot's
  * never-reset optimal_criterion (:193-196), the winner's first layer as the
  * returned state (or the stale one when no leaf wins), the two-non-move stop

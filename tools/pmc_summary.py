@@ -1,11 +1,13 @@
 """Summarise tools/pmc.sh counter passes for the rollout kernel into a JSON
 file bench.py reads for roofline.traffic (--traffic-json).
 
-    python tools/pmc_summary.py gpurun_out/<tag> out.json [algorithmic_bytes] [kernel] [label] [layout]
+    python tools/pmc_summary.py gpurun_out/<tag> out.json [algorithmic_bytes] [kernel] [label] [layout] [sum]
 
 kernel: a substring of the rocprof kernel name (e.g. "k_episode_chain<1, 2, 3"
 for the exchange form); label: the name written to the summary's "kernel"
-field, the key bench.py matches (default: kernel).
+field, the key bench.py matches (default: kernel).  sum: the counters of EVERY
+matching dispatch of a pass added up as one "launch" (a run of several
+kernels, e.g. workload G's lockstep calls: three launches per call).
 
 HBM bytes per launch = 2 x FETCH_SIZE (KB x 1024) + WRITE_SIZE: on gfx950
 FETCH_SIZE counts half the bytes of a 16-B-per-lane streaming read and
@@ -24,12 +26,14 @@ def main():
     kernel = sys.argv[4] if len(sys.argv) > 4 else "k_rollout_argmin_stream"
     label = sys.argv[5] if len(sys.argv) > 5 else kernel
     layout = sys.argv[6] if len(sys.argv) > 6 else "soa"   # the controls' layout of the runs
+    whole_run = len(sys.argv) > 7 and sys.argv[7] == "sum"
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     for f in sorted(glob.glob(os.path.join(root, "pmc*", "p_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
             if kernel not in r["Kernel_Name"]:
                 continue
-            per[r["Counter_Name"]][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
+            key = (f,) if whole_run else (f, r["Dispatch_Id"])
+            per[r["Counter_Name"]][key] += float(r["Counter_Value"])
     med = {}
     for name, d in per.items():
         xs = sorted(d.values())

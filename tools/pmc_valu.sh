@@ -13,11 +13,11 @@ for spec in "chain|1000000 10 chain 20 4|k_episode_chain|160e6" \
             "gen|1000000 10 generated 20 1|k_rollout_generated|0" \
             "ft|0 0 fulltree 6 1|k_ft_leaves|0" \
             "episodes_R|1000 1000 tree_episodes 1 1|k_episodes_run|0" \
-            "ftepisodes_G|1000 50 ft_episodes 1 1|k_ft_episodes_run|0"; do
-  IFS='|' read name args kern algo <<< "$spec"
+            "ftepisodes_G|1000 50 ft_episodes 1 1|k_ftl_|0|sum"; do
+  IFS='|' read name args kern algo mode <<< "$spec"
   mkdir -p $OUT/$name
   timeout -k 10 120 rocprofv3 --pmc $CNT --output-format csv -d $OUT/$name/pmc1 -o p -- python3 tools/prof_kernel.py $args > $OUT/$name/pmc1.log 2>&1 || { echo "$name failed"; tail -5 $OUT/$name/pmc1.log; exit 1; }
-  python3 tools/pmc_summary.py $OUT/$name $OUT/$name.json $algo $kern > /dev/null || exit 1
+  python3 tools/pmc_summary.py $OUT/$name $OUT/$name.json $algo $kern $kern soa $mode > /dev/null || exit 1
 done
 python3 - <<PY
 import json
