@@ -4,8 +4,9 @@ sources (the shipped sources carry none), then one chained step among
 back-to-back ones, decoded per phase.
 
     python tools/chain_timeline.py build            # -> tools/tl_variant.so (CPU)
-    python tools/chain_timeline.py run N_CAND N [p2p]   # on the GPU box (p2p: the
-                                                    # one-rank P2P exchange form)
+    python tools/chain_timeline.py run N_CAND N [p2p|tiled]   # on the GPU box (p2p: the
+                                                    # one-rank P2P exchange form; tiled: the
+                                                    # bench default's tiled batches)
 
 Block 0 (completion of step k-1): entry, records loaded + lane minima, wave
 arg-min, block winner (after the barrier), winner re-rolled (emit_winner),
@@ -102,8 +103,8 @@ def build():
          f"                           lc);\n  {b0(1)}\n  if (static_cast<int>(threadIdx.x) < world)"),
         ("  post_candidate(s_peers, s_rank, world, prev, slot, n_steps, lc);\n",
          f"  post_candidate(s_peers, s_rank, world, prev, slot, n_steps, lc);\n  {b0(2)}\n"),
-        ("      wait_mailbox(S, mb, prev, slot, world, n_steps, s_err ? 0ull : kPeerWaitTicks);\n",
-         "      wait_mailbox(S, mb, prev, slot, world, n_steps, s_err ? 0ull : kPeerWaitTicks);\n"
+        ("      wait_mailbox(S, mb, prev, slot, world, n_steps, s_err == 5u ? 0ull : kPeerWaitTicks);\n",
+         "      wait_mailbox(S, mb, prev, slot, world, n_steps, s_err == 5u ? 0ull : kPeerWaitTicks);\n"
          f"  {b0(3)}\n"),
         ("               kPubWords, publish_epoch);\n  emit_winner_tail",
          f"               kPubWords, publish_epoch);\n  {b0(8)}\n  emit_winner_tail"),
@@ -159,7 +160,10 @@ def run(n, ns, mode="chain"):
     eng = Expansion("cuda:0")
     V = torch.tensor(mmt.vector_of_velocities(0.5), dtype=torch.float64, device="cuda")
     B = torch.tensor(mmt.vector_of_beta_angles(0.0), dtype=torch.float64, device="cuda")
-    pool = [eng.sample_controls(V, B, n, ns, 0x5EED0000 + i) for i in range(8)]
+    if mode == "tiled":   # the bench default's MPC_LAYOUT_TILED batches
+        pool = [eng.sample_controls_tiled(V, B, n, ns, 0x5EED0000 + i) for i in range(8)]
+    else:
+        pool = [eng.sample_controls(V, B, n, ns, 0x5EED0000 + i) for i in range(8)]
     p2p = mode == "p2p"
     ep = DeviceEpisode(eng, n, ns, integrator="rect+cum", chain=True, log_capacity=8192,
                        exchange=p2p, p2p=p2p)

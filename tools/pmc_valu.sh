@@ -5,6 +5,7 @@
 # default for comparison.  Output: gpurun_out/$TAG/<name>/pmc1 + summaries.
 set -o pipefail
 OUT=gpurun_out/${TAG:-valu}
+export MPC_LAYOUT=tiled   # the chained step on the bench default's tiled batches
 mkdir -p $OUT
 export TMPDIR=/tmp
 CNT="SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_WAVES"
