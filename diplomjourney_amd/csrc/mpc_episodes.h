@@ -150,6 +150,122 @@ __device__ __forceinline__ void const_pair_cost(const Consts& K, const double (&
     const_pair_cost_l<INTEG, ROT, false, NS>(K, v, b, n_steps, cst);
 }
 
+// The step's winner (constant controls v, b) re-derived by ONE lane with the
+// rollout's own per-candidate recurrence — rollout_candidate_l's operations,
+// the core form or, for a flagged candidate, the safe form — its layer states
+// 0..2 (clamped to the horizon) into w.tr: the same bits as emit_winner's
+// block-wide re-roll for the direct and rotation heading forms, without its
+// barriers (kRotCum, whose sums run scaled, keeps emit_winner).
+template <int INTEG, int ROT, bool PL2>
+__device__ inline void const_winner_states_l(const Consts& K, double v, double b, int n_steps,
+                                             Winner& w) {
+  static_assert(ROT != kRotCum, "kRotCum winners are re-rolled by emit_winner");
+  auto keep = [&](int st, double x, double y, double ph) {
+    // (constant indices only: a dynamically indexed w.tr would live in scratch)
+    if (st == 0) {
+      w.tr[0][0] = x, w.tr[0][1] = y, w.tr[0][2] = ph;
+    } else if (st == 1) {
+      w.tr[1][0] = x, w.tr[1][1] = y, w.tr[1][2] = ph;
+    } else if (st == 2) {
+      w.tr[2][0] = x, w.tr[2][1] = y, w.tr[2][2] = ph;
+    }
+  };
+  double x, y, ph, s, c;
+  step_start<ROT>(K, x, y, ph, s, c);
+  bool bad = false;
+  for (int st = 0; st < n_steps; ++st) {
+    step_core<INTEG, ROT, PL2>(x, y, ph, s, c, v, b, K, bad);
+    keep(st, x, y, ph);
+  }
+  if (bad) {
+    x = K.x;
+    y = K.y;
+    ph = K.phi;
+    for (int st = 0; st < n_steps; ++st) {
+      step_safe<INTEG>(x, y, ph, v, b, K);
+      keep(st, x, y, ph);
+    }
+  }
+  for (int k = n_steps; k < 3; ++k)   // a horizon below 3: the last layer repeated
+    for (int q = 0; q < 3; ++q) {
+      const double last = n_steps == 1 ? w.tr[0][q] : w.tr[1][q];
+      if (k == 1) w.tr[1][q] = last;
+      if (k == 2) w.tr[2][q] = last;
+    }
+}
+
+// The same states for the direct heading form (ROT = 0), lane-parallel over
+// the steps, by wave 0 (all 64 lanes, n_steps <= 64): the control is constant,
+// so lane s forms its step's heading phi_s = phi + dphi (+ dphi ...) with
+// exactly the serial chain's additions, its sin / cos and (QK21) position
+// increments; lane 0 then only sums them in the serial order (QK21: x + inc;
+// RECT: the fused fma(v h, cos, x)) — the serial recurrence's bits, its
+// dependent chain cut from n_steps x (sin/cos + quadratures) to one.  A
+// flagged candidate (|beta| > kTanMax, |phi_s| > kFastMax) takes lane 0's
+// serial path (const_winner_states_l: the core form, then the safe one).
+template <int INTEG, bool PL2>
+__device__ inline void wave_winner_states_l(const Consts& K, double v, double b, int n_steps,
+                                            Winner& w) {
+  const int lane = threadIdx.x & 63;
+  double ph = K.phi, sn = 0.0, cs = 0.0, ix = 0.0, iy = 0.0;
+  bool bad = !(fabs(b) <= trig::kTanMax);
+  const double t = trig::tan_small(b);
+  double dphi, vh = 0.0;
+  if constexpr (PL2 && INTEG == MPC_INTEG_RECT) {
+    vh = v * K.h;
+    dphi = (vh * K.inv_L) * t;                                 // step_core's form
+  } else {
+    const double wv = PL2 ? v * K.inv_L : v / K.L;
+    dphi = heading_incr<INTEG>(wv, t, K);
+  }
+  if (lane < n_steps) {
+    for (int j = 0; j <= lane; ++j) ph = ph + dphi;
+    bad |= !(fabs(ph) <= trig::kFastMax);
+    trig::sincos_core(ph, &sn, &cs);
+    if constexpr (INTEG != MPC_INTEG_RECT) {
+      ix = quad_const<INTEG>(v * cs, K);                      // position_step's increment
+      iy = quad_const<INTEG>(v * sn, K);
+    }
+  }
+  const bool any_bad = __ballot(lane < n_steps && bad) != 0;
+  if (lane != 0) return;
+  if (any_bad) {
+    const_winner_states_l<INTEG, 0, PL2>(K, v, b, n_steps, w);
+    return;
+  }
+  auto rl = [](double val, int src) {
+    const uint64_t u = static_cast<uint64_t>(__double_as_longlong(val));
+    const uint32_t lo = __builtin_amdgcn_readlane(static_cast<int>(u), src);
+    const uint32_t hi = __builtin_amdgcn_readlane(static_cast<int>(u >> 32), src);
+    return __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | lo));
+  };
+  double x = K.x, y = K.y;
+  for (int st = 0; st < n_steps; ++st) {
+    if constexpr (INTEG == MPC_INTEG_RECT) {
+      const double vhs = PL2 ? vh : v * K.h;                  // = position_step<RECT>
+      x = fma(vhs, rl(cs, st), x);
+      y = fma(vhs, rl(sn, st), y);
+    } else {
+      x = x + rl(ix, st);
+      y = y + rl(iy, st);
+    }
+    const double p = rl(ph, st);
+    if (st == 0) {
+      w.tr[0][0] = x, w.tr[0][1] = y, w.tr[0][2] = p;
+    } else if (st == 1) {
+      w.tr[1][0] = x, w.tr[1][1] = y, w.tr[1][2] = p;
+    } else if (st == 2) {
+      w.tr[2][0] = x, w.tr[2][1] = y, w.tr[2][2] = p;
+    }
+  }
+  for (int k = n_steps; k < 3; ++k)
+    for (int q = 0; q < 3; ++q) {
+      const double last = n_steps == 1 ? w.tr[0][q] : w.tr[1][q];
+      if (k == 1) w.tr[1][q] = last;
+      if (k == 2) w.tr[2][q] = last;
+    }
+}
+
 // Block r = robot r: up to max_calls MPC steps of its episode (fewer if it
 // ends).  log: [n][cap] ring per robot; progress (optional): {calls, stop,
 // candidates} per robot after the launch.
@@ -256,20 +372,55 @@ __global__ __launch_bounds__(NT, PAIR ? 2 : kEpisodesWaves) void k_episodes_run(
       cands += n_grid;
     }
     __syncthreads();
-    // the winner's controls (constant over the horizon) staged for its re-roll
     const uint64_t bk = s_bk;
     const int64_t bi = s_bi;
-    if (bk != ~0ull && threadIdx.x < n_steps) {
-      lds.pv[threadIdx.x] = s_v[bi / nb];
-      lds.pb[threadIdx.x] = s_b[bi % nb];
+    // (in LDS: thread 0's private copy spilled to scratch, a memory round
+    // trip per field on the step's serial path)
+    __shared__ Winner s_win;
+    Winner& win = s_win;
+    if constexpr (ROT != kRotCum) {
+      // wave 0 re-derives the winner itself (wave_winner_states_l for the
+      // direct heading form, one lane's const_winner_states_l for the
+      // rotation form): no block barriers
+      if (threadIdx.x < 64) {
+        if (threadIdx.x == 0) {
+          win.n_steps = n_steps;
+          win.cost = bk == ~0ull ? __builtin_inf() : key_cost(bk);
+          win.index = bk == ~0ull ? -1 : bi;
+          win.found = bk != ~0ull && key_cost(bk) < incumbent ? 1 : 0;
+        }
+        if (bk != ~0ull) {
+          const double wv = s_v[bi / nb], wb = s_b[bi % nb];
+          if (threadIdx.x == 0) {
+            win.v = wv;
+            win.beta = wb;
+          }
+          if constexpr (ROT == 0) {
+            if (K.L_pow2)
+              wave_winner_states_l<INTEG, true>(K, wv, wb, n_steps, win);
+            else
+              wave_winner_states_l<INTEG, false>(K, wv, wb, n_steps, win);
+          } else if (threadIdx.x == 0) {
+            if (K.L_pow2)
+              const_winner_states_l<INTEG, ROT, true>(K, wv, wb, n_steps, win);
+            else
+              const_winner_states_l<INTEG, ROT, false>(K, wv, wb, n_steps, win);
+          }
+        }
+      }
+    } else {
+      // the winner's controls (constant over the horizon) staged for its re-roll
+      if (bk != ~0ull && threadIdx.x < n_steps) {
+        lds.pv[threadIdx.x] = s_v[bi / nb];
+        lds.pb[threadIdx.x] = s_b[bi % nb];
+      }
+      // (v / b: the staged controls again, never read since pre_v / pre_b are
+      // given — null constants there crash hipcc 7.2's inliner, which also
+      // sees k_finalize's call of the same instantiation)
+      emit_winner<INTEG, ROT>(K, lds.pv, lds.pb, 1, n_steps, bk, bi, bi, incumbent, &s_out,
+                              &lds, &win, lds.pv, lds.pb, false);
     }
-    Winner win;
-    // (v / b: the staged controls again, never read since pre_v / pre_b are
-    // given — null constants there crash hipcc 7.2's inliner, which also
-    // sees k_finalize's call of the same instantiation)
-    emit_winner<INTEG, ROT>(K, lds.pv, lds.pb, 1, n_steps, bk, bi, bi, incumbent, &s_out, &lds,
-                            &win, lds.pv, lds.pb, false);
-    if (threadIdx.x == 0) {   // (emit_winner ended with a barrier)
+    if (threadIdx.x == 0) {   // (emit_winner, if it ran, ended with a barrier)
       EpisodeHead H;
       __builtin_memcpy(&H, s_head, sizeof(EpisodeHead));
       episode_advance<false>(c, H, *reinterpret_cast<StaleTraj*>(&s_head[kHeadWords]), win,

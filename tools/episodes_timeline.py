@@ -51,10 +51,10 @@ def build(src=None):
          f"    {mark(0)}\n    const Consts K = uniform_consts(Hs->K);\n"),
         ("    block_argmin<true>(best_k, best_i);\n    if (threadIdx.x == 0) {\n      s_bk = best_k;",
          f"    {mark(1)}\n    block_argmin<true>(best_k, best_i);\n    if (threadIdx.x == 0) {{\n      s_bk = best_k;"),
-        ("    // the winner's controls (constant over the horizon) staged for its re-roll\n",
-         f"    {mark(2)}\n    // the winner's controls (constant over the horizon) staged for its re-roll\n"),
-        ("    if (threadIdx.x == 0) {   // (emit_winner ended with a barrier)\n",
-         f"    {mark(3)}\n    if (threadIdx.x == 0) {{   // (emit_winner ended with a barrier)\n"),
+        ("    const uint64_t bk = s_bk;\n    const int64_t bi = s_bi;\n",
+         f"    {mark(2)}\n    const uint64_t bk = s_bk;\n    const int64_t bi = s_bi;\n"),
+        ("    if (threadIdx.x == 0) {   // (emit_winner, if it ran, ended with a barrier)\n",
+         f"    {mark(3)}\n    if (threadIdx.x == 0) {{   // (emit_winner, if it ran, ended with a barrier)\n"),
         ("      s_calls += 1;\n    }\n",
          f"      s_calls += 1;\n    }}\n    {mark(4)}\n"),
         ("          [threadIdx.x] = reinterpret_cast<const uint64_t*>(&s_log)[threadIdx.x];\n  }\n",
