@@ -1252,17 +1252,22 @@ __global__ __launch_bounds__(kBlock) void k_episode_p2p_flush(
                            index_base, out, log, cap, 0u);
 }
 
-// Launch bound of the chained kernel (waves per SIMD).  The one-GPU form fits
-// 6 (80 VGPRs, no scratch; its LDS fits 6 blocks per CU since block 0's
-// re-roll borrows the idle control ring); the exchange and P2P forms run 5
+// Launch bound of the chained kernel (waves per SIMD).  The one-GPU form runs
+// 5 since round 6 (87 VGPRs, no scratch): at 6 it held 80 VGPRs with 4 spilled
+// (12 B of scratch per lane) and ran 0.2-0.6 us slower per launch at config C
+// and 0.7 us at D (same-box A/Bs, profiles/r06/ab_chain_waves.txt); the
+// exchange and P2P forms run 5
 // (at 6 they keep scratch: the P2P form spilled the work-item id at entry, a
 // 4-B store per lane in EVERY wave — 2 MB of writes per config-C launch, the
 // round-4 traffic excess; measured, 3 interleaved pairs each: exchange 36.73
 // (6 waves) vs 36.31 us, profiles/r04/exchange_waves_ab.txt; P2P 31.17-31.47
 // vs 30.83-31.11 us, profiles/r05/p2p_waves_ab.txt).
+#ifndef MPC_CHAIN_FIN_WAVES
+#define MPC_CHAIN_FIN_WAVES 5
+#endif
 template <int MODE>
 constexpr int chain_waves() {
-  return MODE == kChainFin ? 6 : 5;
+  return MODE == kChainFin ? MPC_CHAIN_FIN_WAVES : 5;
 }
 
 // PL2 (wheelbase a power of two) is a template parameter, not a runtime

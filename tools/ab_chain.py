@@ -35,9 +35,12 @@ def child():
             padded.append((buf[:ns * n].view(ns, n), buf[ns * n:2 * ns * n].view(ns, n), buf))
         pool = [(v, b) for v, b, _ in padded]
         keep = padded   # noqa: F841 (holds the buffers)
+    tpool = pool
+    if os.environ.get("AB_TILED"):   # the bench default's MPC_LAYOUT_TILED batches
+        tpool = [eng.sample_controls_tiled(V, B, n, ns, 0x5EED0000 + i) for i in range(8)]
     ep = DeviceEpisode(eng, n, ns, integrator="rect+cum", chain=True, log_capacity=8192)
     out = {}
-    for name, fn in (("chain", lambda i: ep.step(controls=pool[i % 8])),
+    for name, fn in (("chain", lambda i: ep.step(controls=tpool[i % 8])),
                      ("stream", lambda i: (setattr(ep, "cur", pool[i % 8]), ep.partials()))):
         for i in range(300):
             fn(i)
