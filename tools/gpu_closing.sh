@@ -45,6 +45,6 @@ done
 step bench_qk21 300 bash -c "python bench.py --cpu-seconds 0 --no-second-pass --parity-steps 0 --no-config-d --integrator qk21 > $OUT/bench_qk21.json 2> $OUT/bench_qk21.err"
 step bench_exchange 300 bash -c "python bench.py --cpu-seconds 0 --no-second-pass --parity-steps 0 --no-config-d --exchange > $OUT/bench_exchange.json 2> $OUT/bench_exchange.err"
 step bench_exchange_rccl 300 bash -c "python bench.py --cpu-seconds 0 --no-second-pass --parity-steps 0 --no-config-d --exchange --exchange-mode rccl > $OUT/bench_exchange_rccl.json 2> $OUT/bench_exchange_rccl.err"
-step overlap_exit 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $OUT/overlap_exit -o run -- python3 bench.py --exchange --overlap-exchange --cpu-seconds 0 --no-second-pass --parity-steps 0 --no-config-d --steps 20 --warmup 5
+step overlap_exit 300 bash -c "rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $OUT/overlap_exit -o run -- python3 bench.py --exchange --overlap-exchange --cpu-seconds 0 --no-second-pass --parity-steps 0 --no-config-d --steps 20 --warmup 5 > $OUT/overlap_exit.log 2>&1"
 fi
 echo "[closing] done" >&2
