@@ -151,6 +151,11 @@ def parse():
     ap.add_argument("--no-chain", action="store_true",
                     help="separate selection launch per step instead of chained steps "
                          "(mpc_episode_chain_step: the step's launch completes the previous step)")
+    ap.add_argument("--step-form", default="chain", choices=["run", "chain"],
+                    help="one-GPU chained episode (rect+cum, resident batches): run = the K "
+                         "steps as ONE persistent launch per 64 steps (mpc_episode_run: step "
+                         "k+1 streams while step k is selected, no per-step kernel boundary, "
+                         "no closing flush); chain = one chained launch per step + the flush")
     ap.add_argument("--no-graph", action="store_true",
                     help="time eagerly launched steps instead of a HIP graph replay")
     ap.add_argument("--exchange", action="store_true",
@@ -592,14 +597,23 @@ def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
     # over the gathered candidates and collects this rank's) or the rollout kernel
     chained = not exchange and getattr(ep, "chain", False) and inputs == "resident"
     xchg_chain = exchange and getattr(ep, "chain", False) and inputs == "resident"
-    kernel = ("k_episode_chain" if chained else (P2P_KERNEL if p2p else XCHG_KERNEL)
-              if xchg_chain
+    # one GPU: the K steps as one persistent run (mpc_episode_run) by default
+    run_form = chained and args.step_form == "run" and hasattr(ep, "run")
+    kernel = ("k_episode_run" if run_form else "k_episode_chain" if chained
+              else (P2P_KERNEL if p2p else XCHG_KERNEL) if xchg_chain
               else "k_rollout_argmin_stream")
-    main_run = run_steps(args, ep, pool, use_graph, world, device)
+    main_run = run_steps(args, ep, pool, use_graph, world, device, run_form=run_form)
     use_graph = main_run["graph"]
     kern_ms = main_run["kernel_in_step_ms"]
     sustained_ms = None
-    if (chained or (xchg_chain and p2p)) and use_graph:
+    if run_form and use_graph:
+        # the run's device time per step inside the timed replay; sustained:
+        # a 200-step run replayed (reported beside it)
+        kern_ms = main_run["kernel_timed_ms"]
+        sustained_ms = None if sub else run_pass(ep, pool)
+    elif run_form:
+        kern_ms = run_pass(ep, pool)
+    elif (chained or (xchg_chain and p2p)) and use_graph:
         # one launch per step, the K of the timed region back to back: HIP
         # events around them inside the timed replay
         kern_ms = main_run["kernel_timed_ms"]
@@ -701,21 +715,23 @@ def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
                    "launch": (("hipGraph of the K steps" + (" incl. the RCCL all_gather"
                                                             if exchange and not p2p else ""))
                               if use_graph else "eager"),
-                   "step_launches": (("chained: rollout of step k + completion of step k-1 in "
-                                      "one launch" + (" (selection over the gathered candidates "
-                                                      "of step k-1; the launch also collects "
-                                                      "this rank's candidate of step k), "
-                                                      + ("which block 0 stores into every rank's "
-                                                         "mailbox (peer stores; no collective)"
-                                                         if p2p else "then the all_gather")
-                                                      if exchange else "")
-                                      + (" on a side stream beside the next launch, whose "
-                                         "block 0 waits for its device-side mark; launches on "
-                                         "a CU-masked stream (1 CU per XCD left to the "
-                                         "collective)" if overlap else ""))
-                                     if chain_step
-                                     else "rollout, then selection" + (
-                                         " + all_gather + advance" if exchange else "")),
+                   "step_launches": (
+                       "persistent run: the K steps in ONE launch per 64 steps "
+                       "(mpc_episode_run) — units (step, 512-candidate tile) claimed in order, "
+                       "step k+1 streaming while block 0 selects and applies step k, the last "
+                       "step completed inside the launch" if run_form else
+                       ("chained: rollout of step k + completion of step k-1 in one launch"
+                        + (" (selection over the gathered candidates of step k-1; the launch "
+                           "also collects this rank's candidate of step k), "
+                           + ("which block 0 stores into every rank's mailbox (peer stores; "
+                              "no collective)" if p2p else "then the all_gather")
+                           if exchange else "")
+                        + (" on a side stream beside the next launch, whose block 0 waits for "
+                           "its device-side mark; launches on a CU-masked stream (1 CU per XCD "
+                           "left to the collective)" if overlap else ""))
+                       if chain_step
+                       else "rollout, then selection" + (
+                           " + all_gather + advance" if exchange else "")),
                    "parallelism": f"candidate-sharded x{world}" + (
                        (", 536-B candidates by peer stores/step" if p2p
                         else ", all_gather(536 B candidates)/step" if chain_step
@@ -734,7 +750,10 @@ def bench_episode(args, wl, eng, rank, world, device, cpu, sub=False):
                          else "all_gather (gloo)")),
         "chain_error": chain_err,
         "kernel_ms": kern_ms, "kernel_in_step_ms": main_run["kernel_in_step_ms"],
-        "kernel_ms_note": ("device time per step launch inside the timed region (HIP events "
+        "kernel_ms_note": ("device time per step inside the timed region (HIP events around "
+                           "the timed graph replay of the K-step run, over K)" if run_form and
+                           use_graph else
+                           "device time per step launch inside the timed region (HIP events "
                            "around the timed graph replay, minus the closing flush's own "
                            "duration %.4f ms, over K)" % main_run["flush_ms"]
                            if (chained or (xchg_chain and p2p)) and use_graph
@@ -830,9 +849,12 @@ def parity_pass(args, eng, ep, pool, rank, world, device):
     for k, v in sched.items():
         setattr(fresh.cfg, k, v)
     fresh.reset()                        # the state takes the schedule
-    for i in range(K):
-        fresh.step(controls=pool[i % nb])
-    fresh.flush()
+    if world == 1 and not ep.exchange and args.step_form == "run":
+        fresh.run([pool[i % nb] for i in range(K)])    # the bench's persistent run
+    else:
+        for i in range(K):
+            fresh.step(controls=pool[i % nb])
+        fresh.flush()
     log = fresh.read_log()
     cfg = fresh.cfg
     finish_episode(fresh)
@@ -1091,7 +1113,7 @@ LAYOUT_DOC = {
 }
 
 
-def run_steps(args, ep, pool, use_graph, world, device):
+def run_steps(args, ep, pool, use_graph, world, device, run_form=False):
     """Warmup, the timed K steps, then the eager latency passes.
 
     With a graph (the default): the K steps — and a chained episode's closing
@@ -1112,10 +1134,23 @@ def run_steps(args, ep, pool, use_graph, world, device):
     from diplomjourney_amd.episode import percentile
 
     def step(i, events=None):
-        if pool is None:
+        if run_form:                       # one complete step: a run of one
+            if events:
+                events[0].record()
+            ep.run([pool[i % len(pool)]])
+            if events:
+                events[1].record()
+        elif pool is None:
             ep.step(events=events)
         else:
             ep.step(events=events, controls=pool[i % len(pool)])
+
+    def steps_k():
+        if run_form:                       # the K steps: ONE persistent run
+            ep.run([pool[i % len(pool)] for i in range(args.steps)])
+        else:
+            for i in range(args.steps):
+                step(i)
 
     flush = getattr(ep, "flush", lambda: None)   # completes a chained step left pending
     Ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
@@ -1129,8 +1164,7 @@ def run_steps(args, ep, pool, use_graph, world, device):
         try:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                for i in range(args.steps):
-                    step(i)
+                steps_k()
                 flush()                      # the K-th step completes inside the graph
         except Exception as e:   # capture refused (e.g. by the collective): launch eagerly
             print(f"bench: graph capture failed ({type(e).__name__}: {e}); eager launches",
@@ -1146,8 +1180,7 @@ def run_steps(args, ep, pool, use_graph, world, device):
             graph.replay()
             ep.steps_enqueued += args.steps
         else:
-            for i in range(args.steps):
-                step(i)
+            steps_k()
             flush()
 
     # untimed: the clock ramp. At least 300 steps and ramp_seconds of wall
@@ -1435,6 +1468,28 @@ def chain_pass(ep, pool, reps=200, warm=200):
     # warm + 2 replays (or the eager fallback's reps) of real steps ran
     ep.steps_enqueued = n0 + warm + (2 * reps if how == "graph" else reps)
     return ms
+
+
+def run_pass(ep, pool, reps=200, warm=2):
+    """The persistent run sustained: ONE run of REPS steps rotating over the
+    resident batches (ceil(REPS / 64) launches), captured into a HIP graph,
+    replayed WARM times untimed and once between two HIP events; ms per step.
+    The episode goes on."""
+    import torch
+    batches = [pool[i % len(pool)] for i in range(reps)]
+    n0 = ep.steps_enqueued
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ep.run(batches)
+    for _ in range(warm):
+        g.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    ep.steps_enqueued = n0 + (warm + 1) * reps
+    return e0.elapsed_time(e1) / reps
 
 
 def roofline(achieved, bytes_launch, traffic_json, kernel="k_rollout_argmin_stream",

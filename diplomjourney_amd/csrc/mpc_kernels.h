@@ -1023,12 +1023,18 @@ __device__ __forceinline__ bool early_pose_ok(const mpc_episode_config_t& c, con
 // GEN (generated controls, k_rollout_generated): v / b are [n_part][MPC_MAX_STEPS]
 // — the controls of each rollout block's best candidate — instead of the
 // [n_steps][n_cand] candidate arrays; the winner's are those of its block.
-template <int INTEG, int ROT, bool KDEV, int NT, bool SC1, bool GEN = false, bool TILED = false>
+// Src: where the block records come from.  NoRecSrc: `part` / `n_part` as
+// below; otherwise src(k, i) leaves in every thread the lexicographic minimum
+// of its share of the records (the persistent run's selector, which polls the
+// tagged records of the same launch: mpc_run.h).
+struct NoRecSrc {};
+template <int INTEG, int ROT, bool KDEV, int NT, bool SC1, bool GEN = false, bool TILED = false,
+          class Src = NoRecSrc>
 __device__ __forceinline__ void finalize_block(
     const Rec* __restrict__ part, int n_part, const Consts& K, const double* __restrict__ v,
     const double* __restrict__ b, int64_t n_cand, int n_steps, int64_t index_base,
     double incumbent, mpc_result_t* __restrict__ out, const mpc_episode_config_t& ecfg,
-    const EpisodeHook& hook, EmitLds* lds) {
+    const EpisodeHook& hook, EmitLds* lds, const Src& src = Src{}) {
   // One-GPU episode: the episode scalars are staged in LDS by wave 1 (one
   // 8-B vector load per lane, issued after its record loads) and updated by
   // thread 0 once the winner is known.  (Loading them into thread 0's SGPRs
@@ -1052,7 +1058,9 @@ __device__ __forceinline__ void finalize_block(
   const bool stage = KDEV && hook.H && threadIdx.x >= 64 && threadIdx.x < 64 + kStagedWords;
   const uint64_t head_word =
       stage ? reinterpret_cast<const uint64_t*>(hook.H)[threadIdx.x - 64] : 0ull;
-  if constexpr (SC1) {
+  if constexpr (!std::is_same_v<Src, NoRecSrc>) {
+    src(k, i);
+  } else if constexpr (SC1) {
     // n_part <= kMaxBlocks = 8 * NT: eight loads per thread, addresses of
     // out-of-range slots clamped to a valid record and their values ignored
     static_assert(kMaxBlocks <= 8 * NT, "load8_rec_sc1 covers 8 records per thread");

@@ -23,6 +23,7 @@
 #include "mpc_episodes.h"
 #include "mpc_fulltree.h"
 #include "mpc_kernels.h"
+#include "mpc_run.h"
 
 namespace mpc {
 namespace {
@@ -187,6 +188,29 @@ int64_t fused_grid(int64_t n_cand) {
     cache[dev] = std::min<int64_t>(static_cast<int64_t>(per_cu) * cus, kMaxBlocks);
   }
   return std::max<int64_t>(1, std::min(cdiv(n_cand, kBlock * CPL), cache[dev]));
+}
+
+// Tile blocks of one run launch: one resident round of the instantiation
+// (occupancy x CUs; more would only queue behind it), at most one per unit.
+template <bool P, bool T>
+int64_t run_tile_blocks(int64_t units) {
+  static int64_t cache[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+  if (cache[dev] == 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, reinterpret_cast<const void*>(&k_episode_run<P, T>), kBlock, 0) !=
+            hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus < 1)
+      cus = 256;
+    // block 0 (the selector) takes one of the slots
+    cache[dev] = std::max<int64_t>(1, static_cast<int64_t>(per_cu) * cus - 1);
+  }
+  return std::max<int64_t>(1, std::min(units, cache[dev]));
 }
 
 // Number of block records the rollout launch for these arguments writes
@@ -675,6 +699,83 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
     tl ? launch(std::true_type{}, std::true_type{}) : launch(std::true_type{}, std::false_type{});
   else
     tl ? launch(std::false_type{}, std::true_type{}) : launch(std::false_type{}, std::false_type{});
+  return last_hip_status();
+}
+
+#ifdef MPC_RUN_STATS
+int mpc_debug_run_stats(unsigned long long* host, int reset) {
+  if (reset) {
+    unsigned long long init[kRunMaxSteps][8];
+    for (int j = 0; j < kRunMaxSteps; ++j)
+      for (int f = 0; f < 8; ++f) init[j][f] = (f == 3) ? ~0ull : 0ull;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_run_tl), init, sizeof(init)) == hipSuccess ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_run_tl), sizeof(g_run_tl)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+size_t mpc_episode_run_workspace_bytes(int64_t n_cand) {
+  if (n_cand < 2) return 0;
+  return run_workspace_bytes(cdiv(n_cand, kBlock * kCplWide));
+}
+
+int mpc_episode_run(const mpc_episode_config_t* cfg, void* state, uint32_t epoch0,
+                    const double* const* v_steps, const double* const* beta_steps, int32_t n_run,
+                    int64_t n_cand, int32_t n_steps, int64_t index_base, int32_t integrator,
+                    void* ws, size_t ws_bytes, mpc_result_t* out, mpc_episode_log_t* log,
+                    int32_t log_capacity, mpc_stream_t stream) {
+  if (check_episode_cfg(cfg) != MPC_OK || !state || n_steps < 1 || n_steps > MPC_MAX_STEPS ||
+      n_cand < 2 || index_base < 0 || log_capacity < 0 || epoch0 == 0 || n_run < 1 ||
+      !v_steps || !beta_steps || !out)
+    return MPC_ERR_ARG;
+  // the run's epochs are epoch0 .. epoch0 + n_run - 1, none of them 0
+  if (static_cast<uint64_t>(epoch0) + static_cast<uint64_t>(n_run) - 1u > 0xFFFFFFFFull)
+    return MPC_ERR_ARG;
+  if (n_cand > 0x7fffffffll) return MPC_ERR_ARG;   // 32-bit local indices in the records
+  if (mode_ok(integrator, true, true) != MPC_OK || !is_cum(integrator)) return MPC_ERR_UNSUPPORTED;
+  for (int32_t j = 0; j < n_run; ++j)
+    if (!v_steps[j] || !beta_steps[j] || !chain_ctl_ok(v_steps[j], beta_steps[j], n_cand, integrator))
+      return MPC_ERR_UNSUPPORTED;
+  if (!ws || ws_bytes < mpc_episode_run_workspace_bytes(n_cand)) return MPC_ERR_WORKSPACE;
+  if (!wall_clock_ok()) return MPC_ERR_UNSUPPORTED;
+  EpisodeState* S = static_cast<EpisodeState*>(state);
+  int e;
+  const bool pl2 = frexp(cfg->L, &e) == 0.5;   // as consts_from_problem decides
+  const bool tl = is_tiled(integrator);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t tiles = cdiv(n_cand, kBlock * kCplWide);
+  for (int32_t j0 = 0; j0 < n_run; j0 += kRunMaxSteps) {
+    const int k = std::min<int32_t>(kRunMaxSteps, n_run - j0);
+    RunArgs ra;
+    memset(&ra, 0, sizeof(ra));
+    for (int j = 0; j < k; ++j) {
+      ra.ctl.v[j] = v_steps[j0 + j];
+      ra.ctl.b[j] = beta_steps[j0 + j];
+    }
+    ra.S = S;
+    ra.ws = ws;
+    ra.out = out;
+    ra.log = log;
+    ra.n_cand = n_cand;
+    ra.index_base = index_base;
+    ra.e0 = epoch0 + static_cast<uint32_t>(j0);
+    ra.K = k;
+    ra.n_steps = n_steps;
+    ra.T = static_cast<int>(tiles);
+    ra.cap = log_capacity;
+    ra.ecfg = *cfg;
+    auto launch = [&](auto pl2_tag, auto tiled_tag) {
+      constexpr bool P = decltype(pl2_tag)::value;
+      constexpr bool T = decltype(tiled_tag)::value;
+      const int64_t grid = 1 + run_tile_blocks<P, T>(tiles * k);
+      k_episode_run<P, T><<<grid, kBlock, 0, st>>>(ra);
+    };
+    if (pl2)
+      tl ? launch(std::true_type{}, std::true_type{}) : launch(std::true_type{}, std::false_type{});
+    else
+      tl ? launch(std::false_type{}, std::true_type{}) : launch(std::false_type{}, std::false_type{});
+    if (hipPeekAtLastError() != hipSuccess) break;
+  }
   return last_hip_status();
 }
 

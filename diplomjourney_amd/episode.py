@@ -655,6 +655,49 @@ class DeviceEpisode:
             self.steps_enqueued += 1
         self._ws.reverse()
 
+    def run(self, batches):
+        """len(batches) COMPLETE MPC steps in one persistent launch per 64
+        (mpc_episode_run, csrc/mpc_run.h): step j over batches[j] — each a
+        resident SoA (v, beta) pair or a tiled tensor, one layout for the run.
+        One GPU, rect+cum, the chained step's controls; the log, the state and
+        `local` (the last step's winner) equal those of the same chained steps
+        and their flush, bit for bit.  A pending chained step is completed
+        first."""
+        if self.exchange:
+            raise ValueError("the persistent run: one GPU (no exchange step)")
+        if self.integrator != "rect+cum" or self.n_local % 2:
+            raise ValueError("the persistent run streams rect+cum candidates, n_local even")
+        batches = list(batches)
+        if not batches:
+            return
+        self.flush()
+        ctls = [self._check_controls(c) for c in batches]
+        tiled = self._is_tiled(ctls[0])
+        if any(self._is_tiled(c) != tiled for c in ctls):
+            raise ValueError("one control layout per run")
+        if not tiled and any(not self._chainable(c) for c in ctls):
+            raise ValueError("SoA controls of a run must be 16-B aligned")
+        ptrs = [self._ptrs(c) for c in ctls]
+        k = len(ptrs)
+        V = (ctypes.c_void_p * k)(*[p[0] for p in ptrs])
+        B = (ctypes.c_void_p * k)(*[p[1] for p in ptrs])
+        if getattr(self, "_run_ws", None) is None:
+            # zeroed once; every run leaves it zeroed (tagged records consumed)
+            self._run_ws = torch.zeros(self.lib.mpc_episode_run_workspace_bytes(self.n_local),
+                                       dtype=torch.uint8, device=self.state.device)
+        # k consecutive nonzero epochs (the published constants' tags)
+        if self._epoch + k >= 0xFFFFFFF0:
+            self._epoch = 0
+        e0 = self._epoch + 1
+        self._epoch += k
+        native.check(self.lib.mpc_episode_run(
+            ctypes.byref(self.cfg), self.state.data_ptr(), e0, V, B, k, self.n_local,
+            self.n_steps, self.lo, ptrs[0][2], self._run_ws.data_ptr(), self._run_ws.numel(),
+            self.local.data_ptr(), self.log.data_ptr(), self.log_capacity, self._stream()),
+            "mpc_episode_run")
+        self.cur = ctls[-1]
+        self.steps_enqueued += k
+
     def _next_epoch(self):
         # nonzero, differs from the last and in parity (the P2P mailbox's two
         # slots alternate: 0xFFFFFFFE is followed by 1)

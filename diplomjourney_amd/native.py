@@ -46,6 +46,7 @@ EXPORTS = (
     "mpc_episode_p2p_flush",
     "mpc_fulltree_episodes_state_bytes", "mpc_fulltree_episodes_reset",
     "mpc_fulltree_episodes_run", "mpc_stream_probe_tiled", "mpc_sample_controls_tiled",
+    "mpc_episode_run_workspace_bytes", "mpc_episode_run",
 )
 
 HIPCC_FLAGS = [
@@ -182,6 +183,12 @@ def lib():
                                          ctypes.c_uint32, _P, _P,
                                          _I64, _I32, _I64, _I32, _P, _P, ctypes.c_size_t, _P,
                                          _P, _P, _P, _I32, _P, _I32, _P]
+    L.mpc_episode_run_workspace_bytes.restype = ctypes.c_size_t
+    L.mpc_episode_run_workspace_bytes.argtypes = [_I64]
+    L.mpc_episode_run.restype = ctypes.c_int
+    L.mpc_episode_run.argtypes = [ctypes.POINTER(MpcEpisodeConfig), _P, ctypes.c_uint32,
+                                  ctypes.POINTER(_P), ctypes.POINTER(_P), _I32, _I64, _I32, _I64,
+                                  _I32, _P, ctypes.c_size_t, _P, _P, _I32, _P]
     L.mpc_episode_exchange_step.restype = ctypes.c_int
     L.mpc_episode_exchange_step.argtypes = [ctypes.POINTER(MpcEpisodeConfig), _P, ctypes.c_uint32,
                                             _P, _P, _I64, _I32, _I64, _I32, _P, ctypes.c_size_t,

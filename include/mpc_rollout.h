@@ -353,6 +353,27 @@ int mpc_episode_chain_step(const mpc_episode_config_t* cfg, void* state, int32_t
                            const double* beta_prev, mpc_result_t* out_prev,
                            const mpc_result_t* gathered, int32_t n_gathered,
                            mpc_episode_log_t* log, int32_t log_capacity, mpc_stream_t stream);
+/* Persistent run (one GPU, integrator MPC_INTEG_RECT | MPC_HEADING_CUMULATIVE,
+ * SoA or MPC_LAYOUT_TILED controls under the chained step's rules): n_run
+ * COMPLETE MPC steps of the episode — step j over the caller-resident controls
+ * v_steps[j] / beta_steps[j] (host arrays of device pointers; tiled: beta =
+ * v + 512) — in ONE launch per MPC_RUN_MAX_STEPS steps (math_mpc's loop,
+ * math_model_tree.py:515-635): step j+1's candidates stream while step j is
+ * selected and applied by the launch's first block (the chained step's
+ * completion, mpc_run.h).  Log records, `out` (the last step's winner) and
+ * the state are those of n_run chained steps + their finalize, bit for bit.
+ * No step may be pending (a chained sequence ends with its finalize first).
+ * epoch0: nonzero; the run uses epochs epoch0 .. epoch0 + n_run - 1 (none 0).
+ * ws: mpc_episode_run_workspace_bytes(n_cand), zeroed once by the caller (the
+ * run leaves it zeroed: graph replays are safe).  A timed-out wait sets chain
+ * error 1 (a tile) or 3 (the selector). */
+#define MPC_RUN_MAX_STEPS 64
+size_t mpc_episode_run_workspace_bytes(int64_t n_cand);
+int mpc_episode_run(const mpc_episode_config_t* cfg, void* state, uint32_t epoch0,
+                    const double* const* v_steps, const double* const* beta_steps, int32_t n_run,
+                    int64_t n_cand, int32_t n_steps, int64_t index_base, int32_t integrator,
+                    void* ws, size_t ws_bytes, mpc_result_t* out, mpc_episode_log_t* log,
+                    int32_t log_capacity, mpc_stream_t stream);
 /* Multi-GPU chained step (same integrator and alignment rules): ONE launch per
  * rank and MPC step, then ONE all_gather of `local` (sizeof(mpc_candidate_t)
  * per rank) by the caller — the all-reduce(min+index) of SURVEY §8e:
