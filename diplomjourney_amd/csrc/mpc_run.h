@@ -331,8 +331,17 @@ struct RunArgs {
 // step loop they spilled to scratch (320 B per lane), and the reloads sat on
 // the selection's serial chain.
 template <bool TILED>
-__device__ __attribute__((noinline)) void run_select_step(const __attribute__((address_space(4))) RunArgs& a,
-                                                int j) {
+__device__ __attribute__((noinline)) void run_select_step(uint64_t args_at, int j_in) {
+  // (a call passes its arguments in VGPRs: the step index and the kernarg
+  // address made uniform again, so that the head's constants and every
+  // pointer read from the arguments stay scalar)
+  const int j = __builtin_amdgcn_readfirstlane(j_in);
+  const uint64_t at =
+      (static_cast<uint64_t>(static_cast<uint32_t>(
+           __builtin_amdgcn_readfirstlane(static_cast<int>(args_at >> 32)))) << 32) |
+      static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(args_at)));
+  const __attribute__((address_space(4))) RunArgs& a =
+      *(const __attribute__((address_space(4))) RunArgs*)at;
   EpisodeState* S = a.S;
   const int T = a.T, K = a.K;
   Rec* part = reinterpret_cast<Rec*>(static_cast<char*>(a.ws) + sizeof(RunHdr));
@@ -366,9 +375,7 @@ __global__ __launch_bounds__(kBlock, MPC_CHAIN_FIN_WAVES) void k_episode_run(Run
     if (threadIdx.x == 0 && (ap->S->h.K.L_pow2 != 0) != PL2) ap->S->chain_error = 2u;
     const int K = ap->K;
     for (int j = 0; j < K; ++j) {
-      ArgPtr aj = ap;
-      asm volatile("" : "+s"(aj));   // laundered: nothing of the arguments lives across steps
-      run_select_step<TILED>(*aj, j);
+      run_select_step<TILED>(reinterpret_cast<uint64_t>(ap), j);
       __syncthreads();   // the head's stores before the next step's staging loads
     }
     // the last step's records, consumed: zero them (the workspace is all zero
