@@ -1375,13 +1375,13 @@ P2P_KERNEL = "k_episode_chain[p2p]"
 # committed PMC summaries (tools/pmc.sh + tools/pmc_summary.py), per kernel
 # one per measured size; the one whose algorithmic bytes match is used
 TRAFFIC_JSON = {"k_rollout_argmin_stream": ["r03_traffic_stream.json"],
-                "k_episode_chain": ["r06/traffic_chain_tiled.json",
-                                    "r06/traffic_chain_tiled_D.json",
-                                    "r06/traffic_chain_tiled_Dtotal.json",
+                "k_episode_chain": ["r06_final/traffic_chain_tiled.json",
+                                    "r06_final/traffic_chain_tiled_D.json",
+                                    "r06_final/traffic_chain_tiled_Dtotal.json",
                                     "r04_final/close/traffic_chain.json",
                                     "r05/traffic_chain_D.json"],
                 XCHG_KERNEL: ["r04/traffic_chain_xchg.json"],
-                P2P_KERNEL: ["r06/traffic_chain_p2p_tiled.json",
+                P2P_KERNEL: ["r06_final/traffic_chain_p2p_tiled.json",
                              "r04_final/close/traffic_chain_p2p.json",
                              "r05/traffic_chain_p2p_D.json",
                              "r05/traffic_chain_p2p_tiled_D.json"]}
@@ -1407,15 +1407,15 @@ def traffic_summary(traffic_json, kernel, bytes_launch, layout="soa"):
 # SQ_INSTS_VALU) of each kernel at the size it was measured on:
 # (kernel, integrator) -> (summary, candidates, horizon) — config C, or the
 # S1 = 451 full tree of config F (candidates = leaves)
-VALU_JSON = {("k_episode_chain", "rect+cum"): ("r06/valu/chain.json", 1_000_000, 10),
-             ("k_rollout_argmin_stream", "qk21"): ("r06/valu/qk21.json", 1_000_000, 10),
-             ("k_rollout_generated", "rect+cum"): ("r06/valu/gen.json", 1_000_000, 10),
-             ("k_ft_leaves", "rect+rot"): ("r06/valu/ft.json", 451 ** 3, 3),
+VALU_JSON = {("k_episode_chain", "rect+cum"): ("r06_final/valu/chain.json", 1_000_000, 10),
+             ("k_rollout_argmin_stream", "qk21"): ("r06_final/valu/qk21.json", 1_000_000, 10),
+             ("k_rollout_generated", "rect+cum"): ("r06_final/valu/gen.json", 1_000_000, 10),
+             ("k_ft_leaves", "rect+rot"): ("r06_final/valu/ft.json", 451 ** 3, 3),
              # the device-resident episode drivers: counters of the whole run,
              # keyed (episodes, max_calls) of workloads R and G as the bench runs
              # them (G: every k_ftl_* launch of the run summed)
-             ("k_episodes_run", "qk21"): ("r06/valu/episodes_R.json", 1000, 1000),
-             ("k_ftl_", "rect+rot"): ("r06/valu/ftepisodes_G.json", 1000, 50)}
+             ("k_episodes_run", "qk21"): ("r06_final/valu/episodes_R.json", 1000, 1000),
+             ("k_ftl_", "rect+rot"): ("r06_final/valu/ftepisodes_G.json", 1000, 50)}
 
 
 def valu_roofline(kernel, integrator, ms, n_cand, n_steps, note=None):
