@@ -101,6 +101,41 @@ def test_batched_episodes_argument_validation_without_gpu():
     assert L.mpc_episodes_run(fake, 1, 3, 0, 0, None, 0, None, None) == abi.MPC_OK   # nothing
 
 
+def test_persistent_run_argument_validation_without_gpu():
+    """mpc_episode_run: workspace size and rejected arguments, before any HIP
+    call (epoch 0 or an epoch range past 2^32 - 1, no steps, a horizon out of
+    range, a heading mode other than rect+cum, misaligned or mismatched
+    tiled controls, too small a workspace)."""
+    from diplomjourney_amd.episode import reference_episode_config
+    L = native.lib()
+    n, ns = 20_000, 10
+    tiles = -(-n // 512)
+    wsb = L.mpc_episode_run_workspace_bytes(n)
+    assert wsb == 256 + 2 * tiles * 16 and L.mpc_episode_run_workspace_bytes(1) == 0
+    cfg = reference_episode_config()
+    fake = 0x10000
+    V = (ctypes.c_void_p * 2)(fake, fake + 16 * n)
+    B = (ctypes.c_void_p * 2)(fake + 8 * n * ns, fake + 24 * n)
+    cum = abi.INTEGRATORS["rect+cum"]
+
+    def run(e0=1, k=2, nsteps=ns, integ=cum, v=V, b=B, ws=wsb, nc=n):
+        return L.mpc_episode_run(ctypes.byref(cfg), ctypes.c_void_p(fake), e0, v, b, k, nc,
+                                 nsteps, 0, integ, ctypes.c_void_p(fake), ws, ctypes.c_void_p(fake),
+                                 None, 0, None)
+
+    assert run(e0=0) == abi.MPC_ERR_ARG
+    assert run(e0=0xFFFFFFFF) == abi.MPC_ERR_ARG          # epochs would wrap to 0
+    assert run(k=0) == abi.MPC_ERR_ARG
+    assert run(nsteps=0) == abi.MPC_ERR_ARG
+    assert run(nc=1) == abi.MPC_ERR_ARG
+    assert run(integ=abi.INTEGRATORS["rect+rot"]) == abi.MPC_ERR_UNSUPPORTED
+    Bm = (ctypes.c_void_p * 2)(fake + 8, fake + 24 * n)   # misaligned beta row
+    assert run(b=Bm) == abi.MPC_ERR_UNSUPPORTED
+    Bt = (ctypes.c_void_p * 2)(fake + 8 * 512, fake + 8)  # tiled: beta must be v + 512
+    assert run(integ=cum | abi.MPC_LAYOUT_TILED, b=Bt) == abi.MPC_ERR_UNSUPPORTED
+    assert run(ws=wsb - 1) == abi.MPC_ERR_WORKSPACE
+
+
 def test_workspace_sizes():
     L = native.lib()
     assert L.mpc_workspace_bytes(1, 3) == 16
