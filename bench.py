@@ -24,7 +24,9 @@ host synchronisation inside the loop):
       the rollout/arg-min of step k + the completion of step k-1 (winner
       re-roll + episode update: finishing logic, operator events, next step's
       problem).  --no-chain or another integrator: rollout
-      kernel -> finalize kernel
+      kernel -> finalize kernel.  --step-form run: the K steps as ONE
+      persistent launch per 64 steps (mpc_episode_run; bitwise the chained
+      steps, slower on MI355X: DESIGN.md §6c "Persistent run")
   --inputs sampled  the device sampler first regenerates the candidates on the
       grid around the episode's current control (the reference's per-step
       grid), then the same two kernels
