@@ -508,6 +508,7 @@ def main():
         torch.cuda.empty_cache()
         d_args = argparse.Namespace(**vars(args))
         d_args.candidates_per_gpu = None
+        d_args.dump_log = None               # --dump-log is the main episode's
         d_out, ep, pool = bench_episode(d_args, WORKLOADS["D"], eng, rank, world, device, None,
                                         sub=True)
         out["config_d"] = {k: d_out[k] for k in (
@@ -526,6 +527,7 @@ def main():
         torch.cuda.empty_cache()
         t_args = argparse.Namespace(**vars(args))
         t_args.candidates_per_gpu = -(-D_TOTAL // world)
+        t_args.dump_log = None
         t_out, ep, pool = bench_episode(t_args, WORKLOADS["D"], eng, rank, world, device, None,
                                         sub=True)
         out["config_d_total"] = {k: t_out[k] for k in (
